@@ -1,0 +1,194 @@
+"""torch-tensor wrappers over the librr.so entry points (device memory and
+streams come from PyTorch; all arithmetic is in the HIP kernels).
+
+Shapes follow the engine's layouts: activations NHWC ([N, H, W, C] tensors),
+packed conv weights [c_out, k_packed], descriptors row-major [n, D].
+"""
+
+import ctypes
+
+import torch
+
+from . import _engine as E
+
+
+def _st():
+    return E.stream_ptr()
+
+
+# ---------------------------------------------------------------- extractor ops
+def image_to_nhwc(img, c_pad, dtype, mean=None, std=None):
+    """img: [N, C<=4, H, W] float32 (GPU) -> [N, H, W, c_pad] `dtype`, normalised
+    with (x - mean) / std when mean/std are given (cirtorch/utils/image.py:86-127)."""
+    E.require_gpu(img)
+    img = img.contiguous().float()
+    n, c, h, w = img.shape
+    out = torch.empty((n, h, w, c_pad), dtype=dtype, device=img.device)
+    do = mean is not None
+    m = (ctypes.c_float * 4)(*(list(mean) + [0.0] * (4 - c))[:4]) if do else (ctypes.c_float * 4)()
+    s = (ctypes.c_float * 4)(*(list(std) + [1.0] * (4 - c))[:4]) if do else (ctypes.c_float * 4)(1, 1, 1, 1)
+    E.check(E.lib().rr_image_to_nhwc(E.ptr(img), n, c, h, w, m, s, int(do), E.ptr(out), c_pad,
+                                     E.dtype_code(dtype), _st()), "rr_image_to_nhwc")
+    return out
+
+
+def conv2d_fused(x, w_packed, kh, kw, stride, pad, c_out, scale=None, shift=None, residual=None,
+                 leaky=True, slope=0.01, out_dtype=None, dil=1):
+    """x: [N, H, W, C] -> act(conv(x) * scale + shift (+ residual)) as [N, Ho, Wo, c_out]."""
+    E.require_gpu(x, w_packed)
+    n, h, w, c = x.shape
+    ho = (h + 2 * pad - dil * (kh - 1) - 1) // stride + 1
+    wo = (w + 2 * pad - dil * (kw - 1) - 1) // stride + 1
+    out_dtype = out_dtype or x.dtype
+    y = torch.empty((n, ho, wo, c_out), dtype=out_dtype, device=x.device)
+    flags = 0
+    if scale is not None:
+        flags |= E.RR_CONV_AFFINE
+    if residual is not None:
+        flags |= E.RR_CONV_RESIDUAL
+        assert residual.shape == y.shape and residual.dtype == out_dtype and residual.is_contiguous()
+    d = E.ConvDesc(n=n, h=h, w=w, c_in=c, ho=ho, wo=wo, c_out=c_out, kh=kh, kw=kw, stride=stride, pad=pad,
+                   dil=dil, k_packed=w_packed.shape[1], ldy=c_out,
+                   act=E.RR_ACT_LEAKY if leaky else E.RR_ACT_IDENTITY, slope=slope, flags=flags)
+    E.check(E.lib().rr_conv2d_fused(E.ptr(x), E.ptr(w_packed), E.ptr(scale), E.ptr(shift), E.ptr(residual),
+                                    E.ptr(y), ctypes.byref(d), E.dtype_code(x.dtype), E.dtype_code(out_dtype),
+                                    _st()), "rr_conv2d_fused")
+    return y
+
+
+def maxpool2d(x, k=3, stride=2, pad=1):
+    E.require_gpu(x)
+    n, h, w, c = x.shape
+    ho = (h + 2 * pad - k) // stride + 1
+    wo = (w + 2 * pad - k) // stride + 1
+    y = torch.empty((n, ho, wo, c), dtype=x.dtype, device=x.device)
+    E.check(E.lib().rr_maxpool2d(E.ptr(x), n, h, w, c, k, stride, pad, E.ptr(y), ho, wo, E.dtype_code(x.dtype),
+                                 _st()), "rr_maxpool2d")
+    return y
+
+
+def resize_bilinear(img, scale_factor):
+    """img: [C, H, W] float32 -> bilinear (align_corners=False) resize by
+    scale_factor, output size floor(H*s) x floor(W*s) like
+    nn.functional.interpolate(scale_factor=s) (cirtorch/models/GF_net.py:32-35)."""
+    E.require_gpu(img)
+    img = img.contiguous().float()
+    c, h, w = img.shape
+    ho, wo = int(h * scale_factor), int(w * scale_factor)
+    out = torch.empty((c, ho, wo), dtype=torch.float32, device=img.device)
+    E.check(E.lib().rr_resize_bilinear(E.ptr(img), c, h, w, E.ptr(out), ho, wo, 1.0 / scale_factor,
+                                       1.0 / scale_factor, _st()), "rr_resize_bilinear")
+    return out
+
+
+# ---------------------------------------------------------------- head ops
+def global_pool(x, mode, p=3.0, eps=1e-6):
+    """x: [N, C, H, W] (NCHW-contiguous or channels_last view) -> [N, C] float32."""
+    E.require_gpu(x)
+    n, c, h, w = x.shape
+    if x.is_contiguous(memory_format=torch.channels_last) and not x.is_contiguous():
+        layout = E.RR_NHWC
+    elif x.is_contiguous():
+        layout = E.RR_NCHW
+    else:
+        x = x.contiguous()
+        layout = E.RR_NCHW
+    if layout == E.RR_NHWC and c % 4:
+        x = x.contiguous()
+        layout = E.RR_NCHW
+    if x.dtype not in (torch.float32, torch.bfloat16):
+        x = x.float()
+    out = torch.empty((n, c), dtype=torch.float32, device=x.device)
+    E.check(E.lib().rr_global_pool(E.ptr(x), n, c, h * w, layout, mode, float(p), float(eps), E.ptr(out),
+                                   E.dtype_code(x.dtype), _st()), "rr_global_pool")
+    return out
+
+
+def l2n_rows(x, eps=1e-6):
+    E.require_gpu(x)
+    x = x.contiguous().float()
+    rows = x.shape[0]
+    dim = x.numel() // max(rows, 1)
+    y = torch.empty_like(x)
+    E.check(E.lib().rr_l2n_rows(E.ptr(x), rows, dim, float(eps), E.ptr(y), _st()), "rr_l2n_rows")
+    return y
+
+
+def linear_rows(x, weight, bias=None):
+    E.require_gpu(x, weight, bias)
+    x = x.contiguous().float()
+    weight = weight.contiguous().float()
+    bias = bias.contiguous().float() if bias is not None else None
+    rows, in_dim = x.shape
+    out_dim = weight.shape[0]
+    y = torch.empty((rows, out_dim), dtype=torch.float32, device=x.device)
+    E.check(E.lib().rr_linear_rows(E.ptr(x), rows, in_dim, E.ptr(weight), E.ptr(bias), out_dim, E.ptr(y), _st()),
+            "rr_linear_rows")
+    return y
+
+
+def head_tail(pooled, weight, bias, whiten=True, eps=1e-6):
+    """pooled [N, D] -> L2N(W . L2N(pooled) + b) (global_head.py:59-64), [N, D]."""
+    E.require_gpu(pooled, weight, bias)
+    pooled = pooled.contiguous().float()
+    rows, dim = pooled.shape
+    y = torch.empty_like(pooled)
+    ws = torch.empty(int(E.lib().rr_head_workspace_bytes(rows, dim)) // 4 + 1, dtype=torch.float32,
+                     device=pooled.device) if whiten else None
+    w = weight.contiguous().float() if whiten else None
+    b = bias.contiguous().float() if (whiten and bias is not None) else None
+    E.check(E.lib().rr_head_l2n_whiten_l2n(E.ptr(pooled), rows, dim, E.ptr(w), E.ptr(b), int(bool(whiten)),
+                                           float(eps), E.ptr(y), E.ptr(ws), _st()), "rr_head_l2n_whiten_l2n")
+    return y
+
+
+# ---------------------------------------------------------------- matching
+def knn_workspace_bytes(n_db, nq, d, k, cand=0, dtype=torch.float32):
+    return int(E.lib().rr_knn_workspace_bytes(int(n_db), int(nq), int(d), int(k), int(cand), E.dtype_code(dtype)))
+
+
+def knn_topk(db, db_f32, q, q_f32, k, cand=0, idx_offset=0, workspace=None):
+    """db/q: [n, D] rows in the screening dtype (float32 or bfloat16);
+    db_f32/q_f32: the float32 rows used for the exact re-score.
+    Returns (scores float64 [Q, k], idx int64 [Q, k])."""
+    E.require_gpu(db, db_f32, q, q_f32)
+    assert db.dtype == q.dtype and db_f32.dtype == torch.float32 and q_f32.dtype == torch.float32
+    for t in (db, db_f32, q, q_f32):
+        assert t.is_contiguous()
+    n_db, d = db.shape
+    nq = q.shape[0]
+    need = knn_workspace_bytes(n_db, nq, d, k, cand, db.dtype)
+    if workspace is None or workspace.numel() < need:
+        workspace = torch.empty(need, dtype=torch.uint8, device=db.device)
+    out_s = torch.empty((nq, k), dtype=torch.float64, device=db.device)
+    out_i = torch.empty((nq, k), dtype=torch.int64, device=db.device)
+    E.check(E.lib().rr_knn_topk(E.ptr(db), E.ptr(db_f32), n_db, E.ptr(q), E.ptr(q_f32), nq, d, k, int(cand),
+                                int(idx_offset), E.ptr(out_s), E.ptr(out_i), E.ptr(workspace),
+                                workspace.numel(), E.dtype_code(db.dtype), _st()), "rr_knn_topk")
+    return out_s, out_i
+
+
+def topk_merge(scores, idx, k):
+    """scores/idx: [R, Q, k_in] per-shard lists -> merged [Q, k]."""
+    E.require_gpu(scores, idx)
+    r, nq, k_in = scores.shape
+    out_s = torch.empty((nq, k), dtype=torch.float64, device=scores.device)
+    out_i = torch.empty((nq, k), dtype=torch.int64, device=scores.device)
+    E.check(E.lib().rr_topk_merge(E.ptr(scores.contiguous()), E.ptr(idx.contiguous()), r, nq, k_in, k,
+                                  E.ptr(out_s), E.ptr(out_i), _st()), "rr_topk_merge")
+    return out_s, out_i
+
+
+def fill_unit_rows(rows, d, seed, row0=0, device=None):
+    out = torch.empty((rows, d), dtype=torch.float32, device=device or "cuda")
+    E.check(E.lib().rr_fill_unit_rows(E.ptr(out), int(rows), int(d), ctypes.c_ulonglong(seed), int(row0), _st()),
+            "rr_fill_unit_rows")
+    return out
+
+
+def cast_bf16(x):
+    E.require_gpu(x)
+    x = x.contiguous()
+    y = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+    E.check(E.lib().rr_cast_f32_bf16(E.ptr(x), E.ptr(y), x.numel(), _st()), "rr_cast_f32_bf16")
+    return y

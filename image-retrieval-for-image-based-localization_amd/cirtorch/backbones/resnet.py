@@ -1,0 +1,238 @@
+"""ResNet body on the MI355X engine.
+
+Module tree, parameter names, registry and ``convert`` follow the reference
+``cirtorch/backbones/resnet.py:15-180`` so its state dicts (and torchvision
+ones via ``convert``) load unchanged.  ``forward`` follows the *intended*
+reference semantics — all five stages (the checked-in reference comments out
+mod4/mod5 at ``resnet.py:158-159`` while ``GF_algo._get_level`` needs mod5).
+
+Execution: on first use (and after ``load_state_dict`` / ``.to()`` /
+``set_precision``) the module builds an engine plan — per conv a packed
+[c_out][kh*kw*c_in] weight in the compute dtype plus the folded BN
+scale/shift — and runs the whole body as a chain of librr.so launches:
+
+    image_to_nhwc (normalise + layout) -> stem conv 7x7/2 (+BN+leaky)
+    -> maxpool 3x3/2 -> per block: [proj 1x1 (+BN)] , conv1 (+BN+leaky),
+       conv2 (+BN+leaky), conv3 (+BN + residual + leaky)
+
+Activations stay NHWC in HBM; the returned stage maps are NCHW-shaped
+``channels_last`` views of those buffers (no copies).
+"""
+
+import sys
+from collections import OrderedDict
+from functools import partial
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import _ops
+from ..modules.abn import ABN
+from .misc import ResidualBlock
+
+CONV_PARAMS = ["weight"]
+BN_PARAMS = ["weight", "bias", "running_mean", "running_var"]
+
+_PRECISIONS = {"bf16": torch.bfloat16, "fp32": torch.float32, "float32": torch.float32, "bfloat16": torch.bfloat16}
+
+
+def try_index(scalar_or_list, i):
+    try:
+        return scalar_or_list[i]
+    except TypeError:
+        return scalar_or_list
+
+
+class _ConvStep:
+    __slots__ = ("w", "kh", "kw", "stride", "pad", "c_out", "scale", "shift", "leaky", "slope")
+
+
+class ResNet(nn.Module):
+    """Standard residual network (reference ``resnet.py:15-164``).
+
+    Extra (engine) argument: ``precision`` in {"bf16", "fp32"} — the MFMA
+    operand / activation storage type (accumulation is always float32)."""
+
+    def __init__(self, structure, bottleneck, norm_act=ABN, config=None, classes=0, dilation=1, dropout=None,
+                 caffe_mode=False, precision="bf16"):
+        super().__init__()
+        self.structure = structure
+        self.bottleneck = bottleneck
+        self.dilation = dilation
+        self.dropout = dropout
+        self.caffe_mode = caffe_mode
+        if len(structure) != 4:
+            raise ValueError("Expected a structure with four values")
+        if dilation != 1 and len(dilation) != 4:
+            raise ValueError("If dilation is not 1 it must contain four values")
+        if dilation != 1:
+            raise NotImplementedError("dilated ResNets are out of scope for the MI355X engine")
+        if caffe_mode:
+            raise NotImplementedError("caffe_mode (stem conv bias) is out of scope")
+        if classes != 0:
+            raise NotImplementedError("the classifier head is out of scope (retrieval uses classes=0)")
+
+        layers = [
+            ("conv1", nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)),
+            ("bn1", try_index(norm_act, 0)(64)),
+            ("pool1", nn.MaxPool2d(3, stride=2, padding=1)),
+        ]
+        self.mod1 = nn.Sequential(OrderedDict(layers))
+        in_channels = 64
+        channels = (64, 64, 256) if self.bottleneck else (64, 64)
+        for mod_id, num in enumerate(structure):
+            blocks = []
+            for block_id in range(num):
+                stride = 2 if block_id == 0 and mod_id > 0 else 1
+                blocks.append(("block%d" % (block_id + 1),
+                               ResidualBlock(in_channels, channels, norm_act=try_index(norm_act, mod_id),
+                                             stride=stride, dilation=1)))
+                in_channels = channels[-1]
+            self.add_module("mod%d" % (mod_id + 2), nn.Sequential(OrderedDict(blocks)))
+            channels = [c * 2 for c in channels]
+        self.out_channels = in_channels
+        self.engine_dtype = _PRECISIONS[precision]
+        self._plan = None
+
+    # ------------------------------------------------------------ reference API
+    @staticmethod
+    def _stride_dilation(dilation, mod_id, block_id):
+        d = try_index(dilation, mod_id)
+        s = 2 if d == 1 and block_id == 0 and mod_id > 0 else 1
+        return s, d
+
+    def copy_layer(self, inm, outm, name_in, name_out, params):
+        for param_name in params:
+            outm[name_out + "." + param_name] = inm[name_in + "." + param_name]
+
+    def convert(self, model):
+        """torchvision resnet state dict -> this module's keys (``resnet.py:116-149``)."""
+        out = dict()
+        num_convs = 3 if self.bottleneck else 2
+        self.copy_layer(model, out, "conv1", "mod1.conv1", CONV_PARAMS)
+        self.copy_layer(model, out, "bn1", "mod1.bn1", BN_PARAMS)
+        for mod_id, num in enumerate(self.structure):
+            for block_id in range(num):
+                for conv_id in range(num_convs):
+                    self.copy_layer(model, out, "layer{}.{}.conv{}".format(mod_id + 1, block_id, conv_id + 1),
+                                    "mod{}.block{}.convs.conv{}".format(mod_id + 2, block_id + 1, conv_id + 1),
+                                    CONV_PARAMS)
+                    self.copy_layer(model, out, "layer{}.{}.bn{}".format(mod_id + 1, block_id, conv_id + 1),
+                                    "mod{}.block{}.convs.bn{}".format(mod_id + 2, block_id + 1, conv_id + 1),
+                                    BN_PARAMS)
+                try:
+                    self.copy_layer(model, out, "layer{}.{}.downsample.0".format(mod_id + 1, block_id),
+                                    "mod{}.block{}.proj_conv".format(mod_id + 2, block_id + 1), CONV_PARAMS)
+                    self.copy_layer(model, out, "layer{}.{}.downsample.1".format(mod_id + 1, block_id),
+                                    "mod{}.block{}.proj_bn".format(mod_id + 2, block_id + 1), BN_PARAMS)
+                except KeyError:
+                    pass
+        return out
+
+    # ------------------------------------------------------------ engine plan
+    def set_precision(self, precision):
+        self.engine_dtype = _PRECISIONS[precision]
+        self._plan = None
+        return self
+
+    def refresh_engine(self):
+        """Rebuild packed weights (call after modifying parameters in place)."""
+        self._plan = None
+
+    def _apply(self, fn, *args, **kwargs):
+        self._plan = None
+        return super()._apply(fn, *args, **kwargs)
+
+    def _load_from_state_dict(self, *args, **kwargs):
+        self._plan = None
+        return super()._load_from_state_dict(*args, **kwargs)
+
+    def stem_cin(self):
+        return 8 if self.engine_dtype == torch.bfloat16 else 4
+
+    def _step(self, conv, bn, cin_pad=None, leaky_override=None):
+        st = _ConvStep()
+        w = conv.weight.detach().float()
+        co, ci, kh, kw = w.shape
+        cin_pad = cin_pad or ci
+        wp = w.permute(0, 2, 3, 1)  # co, kh, kw, ci  (k = (kh*KW + kw)*c_in + ci)
+        if cin_pad > ci:
+            wp = F.pad(wp, (0, cin_pad - ci))
+        wp = wp.reshape(co, kh * kw * cin_pad)
+        kp = (wp.shape[1] + 31) // 32 * 32
+        if kp > wp.shape[1]:
+            wp = F.pad(wp, (0, kp - wp.shape[1]))
+        st.w = wp.to(self.engine_dtype).contiguous()
+        st.kh, st.kw = kh, kw
+        st.stride = conv.stride[0]
+        st.pad = conv.padding[0]
+        st.c_out = co
+        st.scale, st.shift = bn.folded()
+        st.leaky, st.slope = bn.slope()
+        if leaky_override is not None:
+            st.leaky = leaky_override
+        return st
+
+    def _build_plan(self):
+        dev = self.mod1.conv1.weight.device
+        if dev.type != "cuda":
+            raise RuntimeError("the MI355X engine runs on the GPU: call .cuda() on the model first")
+        plan = {"stem": self._step(self.mod1.conv1, self.mod1.bn1, cin_pad=self.stem_cin()), "mods": []}
+        for mod_id in range(4):
+            mod = getattr(self, "mod%d" % (mod_id + 2))
+            blocks = []
+            for blk in mod.children():
+                c = blk.convs
+                post_leaky, post_slope = c.bn1.slope()  # post-add activation (misc.py:194-203)
+                if blk.is_bottleneck:
+                    steps = [self._step(c.conv1, c.bn1), self._step(c.conv2, c.bn2), self._step(c.conv3, c.bn3)]
+                else:
+                    steps = [self._step(c.conv1, c.bn1), self._step(c.conv2, c.bn2)]
+                steps[-1].leaky, steps[-1].slope = post_leaky, post_slope
+                proj = self._step(blk.proj_conv, blk.proj_bn, leaky_override=False) if hasattr(blk, "proj_conv") else None
+                blocks.append((steps, proj))
+            plan["mods"].append(blocks)
+        self._plan = plan
+        return plan
+
+    @staticmethod
+    def _conv(t, st, residual=None):
+        return _ops.conv2d_fused(t, st.w, st.kh, st.kw, st.stride, st.pad, st.c_out, st.scale, st.shift,
+                                 residual=residual, leaky=st.leaky, slope=st.slope)
+
+    def forward(self, x, normalize=None):
+        """x: [N, 3, H, W] float32 on the GPU (already normalised unless
+        ``normalize=(mean, std)`` is given, which fuses cirtorch/utils/image.py
+        ``normalize`` into the first kernel).  Returns OrderedDict mod1..mod5."""
+        plan = self._plan or self._build_plan()
+        mean, std = normalize if normalize is not None else (None, None)
+        t = _ops.image_to_nhwc(x, self.stem_cin(), self.engine_dtype, mean, std)
+        t = self._conv(t, plan["stem"])
+        t = _ops.maxpool2d(t, 3, 2, 1)
+        outs = OrderedDict()
+        outs["mod1"] = t
+        for mod_id, blocks in enumerate(plan["mods"]):
+            for steps, proj in blocks:
+                res = self._conv(t, proj) if proj is not None else t
+                y = t
+                for st in steps[:-1]:
+                    y = self._conv(y, st)
+                t = self._conv(y, steps[-1], residual=res)
+            outs["mod%d" % (mod_id + 2)] = t
+        return OrderedDict((k, v.permute(0, 3, 1, 2)) for k, v in outs.items())
+
+
+_NETS = {
+    "18": {"structure": [2, 2, 2, 2], "bottleneck": False},
+    "34": {"structure": [3, 4, 6, 3], "bottleneck": False},
+    "50": {"structure": [3, 4, 6, 3], "bottleneck": True},
+    "101": {"structure": [3, 4, 23, 3], "bottleneck": True},
+    "152": {"structure": [3, 8, 36, 3], "bottleneck": True},
+}
+
+__all__ = []
+for _name, _params in _NETS.items():
+    _net_name = "resnet" + _name
+    setattr(sys.modules[__name__], _net_name, partial(ResNet, **_params))
+    __all__.append(_net_name)

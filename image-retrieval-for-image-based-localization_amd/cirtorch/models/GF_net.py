@@ -1,0 +1,200 @@
+"""ImageRetrievalNet (reference ``cirtorch/models/GF_net.py:10-126``) plus the
+upstream entry points ``scripts/test.py`` imports from this module
+(``init_network``, ``extract_vectors``; ``scripts/test.py:12,105,200,236-238``).
+
+forward(img=PackedSequence, scales=[...]) -> (OrderedDict(ret_loss=None),
+OrderedDict(ret_pred=Tensor[D, N])), with the reference semantics:
+  * multi-scale: per-image bilinear resize (align_corners=False), recursive
+    single-scale extraction, plain mean of the per-scale L2-normalised
+    descriptors, no re-normalisation (``GF_net.py:20-40,74-92``);
+  * pad to the batch's max H, W top-left (``utils/sequence.py``), then
+    normalise (pads become -mean/std, ``random_augmentation.py:102,174``)
+    when an augment object carrying rgb_mean / rgb_std is attached;
+  * body -> ret_algo.inference(head, x) -> D x N.
+"""
+
+from collections import OrderedDict
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from .. import _ops
+from ..algos.GF_algo import globalFeatureAlgo
+from ..backbones import resnet as _resnet
+from ..modules.heads.global_head import globalHead
+from ..utils.parallel import PackedSequence
+from ..utils.sequence import pad_packed_images
+
+OUTPUT_DIM = {"resnet18": 512, "resnet34": 512, "resnet50": 2048, "resnet101": 2048, "resnet152": 2048}
+
+
+class Normalize:
+    """Minimal stand-in for the reference augment object
+    (``RandomAugmentation(rgb_mean, rgb_std)``): eval-time normalisation only,
+    fused by the engine into the first kernel."""
+
+    def __init__(self, rgb_mean=(0.485, 0.456, 0.406), rgb_std=(0.229, 0.224, 0.225)):
+        self.rgb_mean = list(rgb_mean)
+        self.rgb_std = list(rgb_std)
+
+
+class ImageRetrievalNet(nn.Module):
+    def __init__(self, body, ret_algo, ret_head, augment=None):
+        super().__init__()
+        self.augment = augment
+        self.body = body
+        self.ret_algo = ret_algo
+        self.ret_head = ret_head
+        self.meta = {}
+
+    # ----------------------------------------------------------------- helpers
+    def _prepare_pyramid_inputs(self, img, scales):
+        out = []
+        for scale in scales:
+            if scale == 1:
+                out.append(img)
+            else:
+                out.append(PackedSequence([_ops.resize_bilinear(im, scale) for im in img]))
+        return out
+
+    def _normalizer(self):
+        a = self.augment
+        if a is None:
+            return None
+        if hasattr(a, "rgb_mean") and hasattr(a, "rgb_std"):
+            return (list(a.rgb_mean), list(a.rgb_std))
+        raise NotImplementedError("only normalising augment objects (rgb_mean/rgb_std) are supported at eval time")
+
+    @property
+    def pool(self):
+        """upstream ``net.pool`` (``scripts/test.py:137``)."""
+        return self.ret_head.pool
+
+    def meta_repr(self):
+        tmp = "  (meta): dict( \n"
+        for k in ("architecture", "local_whitening", "pooling", "regional", "whitening", "outputdim", "mean", "std"):
+            if k in self.meta:
+                tmp += "     %s: %s\n" % (k, self.meta[k])
+        tmp += "  )\n"
+        return tmp
+
+    # ----------------------------------------------------------------- forward
+    def forward(self, img=None, positive_img=None, negative_img=None, scales=[1], do_augmentaton=False,
+                do_loss=False, do_prediction=True, **varargs):
+        if do_loss:
+            raise NotImplementedError("training (tuple loss) is out of scope for the MI355X engine")
+        if isinstance(img, torch.Tensor):
+            img = PackedSequence(list(img)) if img.dim() == 4 else PackedSequence([img])
+        if len(scales) > 1:
+            preds = []
+            for im in self._prepare_pyramid_inputs(img, scales):
+                _, pred = self.forward(img=im, scales=[1], do_prediction=True, do_loss=False)
+                preds.append(pred["ret_pred"].unsqueeze(0))
+            pred = torch.cat(preds, dim=0).permute(1, 2, 0)
+            pred = nn.functional.avg_pool1d(pred, kernel_size=len(scales)).squeeze(-1)
+            return None, OrderedDict([("ret_pred", pred)])
+
+        padded, valid_size = pad_packed_images(img)
+        x = self.body(padded, normalize=self._normalizer())
+        if do_prediction:
+            ret_pred = self.ret_algo.inference(self.ret_head, x, valid_size)
+        else:
+            ret_pred = None
+        return OrderedDict([("ret_loss", None)]), OrderedDict([("ret_pred", ret_pred)])
+
+    # upstream-style single call: list of [3, H, W] tensors -> D x N
+    def extract(self, images, scales=(1,)):
+        with torch.no_grad():
+            _, pred = self.forward(img=PackedSequence(list(images)), scales=list(scales))
+        return pred["ret_pred"]
+
+
+def make_net(architecture="resnet50", pooling="gem", whitening=True, mean=None, std=None, precision="bf16",
+             p=3.0):
+    """Build body + globalHead + algo the way ``scripts/train_globalF.py:make_model`` does
+    (``:240-356``): leaky_relu(0.01) ABN, GeM(p, 1e-6), L2N, Linear(dim, dim) whitening."""
+    body = _resnet.__dict__[architecture](precision=precision)
+    dim = OUTPUT_DIM[architecture]
+    pname = {"gem": "GeM", "mac": "MAC", "spoc": "SPoC"}[pooling.lower()]
+    params = {"p": p, "eps": 1e-6} if pname == "GeM" else {}
+    head = globalHead(pooling={"name": pname, "params": params}, normal={"name": "L2N", "params": {}}, dim=dim)
+    algo = globalFeatureAlgo(loss=None, min_level=0, fpn_levels=1)
+    if not whitening:
+        algo._head = lambda h, x: h(x, do_whitening=False)
+    augment = Normalize(mean, std) if mean is not None else None
+    net = ImageRetrievalNet(body, algo, head, augment=augment)
+    net.meta = {"architecture": architecture, "pooling": pooling, "local_whitening": False, "regional": False,
+                "whitening": whitening, "mean": list(mean) if mean is not None else None,
+                "std": list(std) if std is not None else None, "outputdim": dim}
+    return net
+
+
+def init_network(params):
+    """Upstream ``init_network(params)`` (``scripts/test.py:105``)."""
+    arch = params.get("architecture", "resnet101")
+    pooling = params.get("pooling", "gem")
+    if params.get("local_whitening", False) or params.get("regional", False):
+        raise NotImplementedError("local whitening / regional pooling are out of scope")
+    if params.get("pretrained", False):
+        # offline build: no ImageNet weights can be fetched; random init instead
+        pass
+    mean = params.get("mean", [0.485, 0.456, 0.406])
+    std = params.get("std", [0.229, 0.224, 0.225])
+    return make_net(arch, pooling, params.get("whitening", False), mean, std,
+                    precision=params.get("precision", "bf16"))
+
+
+def _load_pil(path, imsize, bbx=None):
+    from PIL import Image
+    with open(path, "rb") as f:
+        img = Image.open(f).convert("RGB")
+    if bbx is not None:
+        img = img.crop(bbx)
+    if imsize is not None:
+        img.thumbnail((imsize, imsize), Image.LANCZOS)
+    return img
+
+
+def _to_tensor(img):
+    a = np.asarray(img, dtype=np.float32) / 255.0
+    return torch.from_numpy(a.transpose(2, 0, 1).copy())
+
+
+def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], msp=1, print_freq=10):
+    """Upstream ``extract_vectors`` (``scripts/test.py:200,236-238``): returns a
+    CPU float32 tensor D x len(images).  ``images`` are file paths (loaded with
+    PIL, longest side resized to image_size) or [3, H, W] tensors in [0, 1].
+    ms/msp follow the upstream rule: v = (mean_s f(x_s)^msp)^(1/msp), L2N."""
+    dev = next(net.parameters()).device
+    vecs = torch.zeros(net.meta.get("outputdim", 2048), len(images))
+    normalize_in_net = net.augment is not None and transform is None
+    for i, item in enumerate(images):
+        if isinstance(item, str):
+            pil = _load_pil(item, image_size, bbxs[i] if bbxs is not None else None)
+            x = transform(pil) if transform is not None else _to_tensor(pil)
+        else:
+            x = item
+        x = x.to(dev).float()
+        if not normalize_in_net and transform is None and net.meta.get("mean") is not None:
+            m = torch.tensor(net.meta["mean"], device=dev)[:, None, None]
+            s = torch.tensor(net.meta["std"], device=dev)[:, None, None]
+            x = (x - m) / s
+        saved = net.augment
+        if not normalize_in_net:
+            net.augment = None
+        try:
+            if list(ms) == [1]:
+                v = net.extract([x])[:, 0]
+            else:
+                acc = None
+                for s in ms:
+                    xs = x if s == 1 else _ops.resize_bilinear(x, s)
+                    v = net.extract([xs])[:, 0].pow(msp)
+                    acc = v if acc is None else acc + v
+                v = (acc / len(ms)).pow(1.0 / msp)
+                v = v / v.norm()
+        finally:
+            net.augment = saved
+        vecs[:, i] = v.float().cpu()
+    return vecs

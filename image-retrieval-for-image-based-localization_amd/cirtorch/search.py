@@ -1,0 +1,99 @@
+"""GPU matching: the replacement for the reference's host-side rank
+``scores = np.dot(vecs.T, qvecs); ranks = np.argsort(-scores, axis=0)``
+(``scripts/test.py:247-248``, ``scripts/train_globalF.py:733-734``).
+
+* ``knn(vecs, qvecs, k)``  -> first k ranks (k x Q, int64) and their scores,
+  exactly ordered by (score desc, index asc); scores re-computed in float64.
+* ``rank(vecs, qvecs)``     -> full ranks (N x Q) for mAP evaluation (N <= 8192).
+* ``KnnIndex``              -> a resident database (float32 rows + optional
+  bf16 screening copy) queried many times.
+* ``ShardedIndex``          -> database rows split over the ranks of a
+  torch.distributed group (RCCL on ROCm), per-shard top-k, all-gather of the
+  (score, index) lists, on-GPU merge — bit-identical to the 1-GPU result.
+
+Layouts: the reference keeps descriptors as D x N columns; the engine reads
+row-major [N][D].  ``vecs.t()`` of a D x N column matrix produced by
+``globalHead`` is already a contiguous [N][D] view (no copy).
+"""
+
+import torch
+import torch.distributed as dist
+
+from . import _ops
+
+_PREC = {"fp32": torch.float32, "float32": torch.float32, "bf16": torch.bfloat16, "bfloat16": torch.bfloat16}
+
+
+def _rows(cols):
+    """D x N column matrix (torch or numpy) -> contiguous float32 [N][D] on GPU."""
+    if not torch.is_tensor(cols):
+        cols = torch.from_numpy(cols)
+    rows = cols.t()
+    if not rows.is_cuda:
+        rows = rows.cuda()
+    return rows.float().contiguous()
+
+
+class KnnIndex:
+    def __init__(self, db_rows, precision="fp32", cand=0, idx_offset=0):
+        """db_rows: [N, D] float32 on the GPU (kept by reference, not copied)."""
+        self.db32 = db_rows.float().contiguous()
+        self.dtype = _PREC[precision]
+        self.db = self.db32 if self.dtype == torch.float32 else _ops.cast_bf16(self.db32)
+        self.cand = cand
+        self.idx_offset = idx_offset
+        self._ws = None
+
+    @property
+    def ntotal(self):
+        return self.db32.shape[0]
+
+    def search(self, q_rows, k):
+        q32 = q_rows.float().contiguous()
+        q = q32 if self.dtype == torch.float32 else _ops.cast_bf16(q32)
+        need = _ops.knn_workspace_bytes(self.ntotal, q.shape[0], q.shape[1], k, self.cand, self.dtype)
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(need, dtype=torch.uint8, device=q.device)
+        return _ops.knn_topk(self.db, self.db32, q, q32, k, cand=self.cand, idx_offset=self.idx_offset,
+                             workspace=self._ws)
+
+
+def knn(vecs, qvecs, k, precision="fp32", cand=0):
+    """vecs D x N, qvecs D x Q (reference layout) -> (ranks k x Q int64, scores k x Q float64)."""
+    db = _rows(vecs)
+    q = _rows(qvecs)
+    s, i = KnnIndex(db, precision, cand).search(q, k)
+    return i.t(), s.t()
+
+
+def rank(vecs, qvecs, precision="fp32"):
+    """Full ranking, the GPU equivalent of ``np.argsort(-np.dot(vecs.T, qvecs), axis=0)``."""
+    n = vecs.shape[1]
+    ranks, _ = knn(vecs, qvecs, n, precision=precision, cand=n)
+    return ranks
+
+
+class ShardedIndex:
+    """Database rows [row0, row0 + n_local) of a global matrix live on this
+    rank; ``search`` expects the same queries on every rank (all-gather them
+    first if each rank extracted its own)."""
+
+    def __init__(self, local_rows, row0, precision="bf16", cand=0, group=None):
+        self.local = KnnIndex(local_rows, precision, cand, idx_offset=row0)
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+
+    def search(self, q_rows, k):
+        s, i = self.local.search(q_rows, k)
+        if self.world == 1:
+            return s, i
+        gs = torch.empty((self.world,) + tuple(s.shape), dtype=s.dtype, device=s.device)
+        gi = torch.empty((self.world,) + tuple(i.shape), dtype=i.dtype, device=i.device)
+        dist.all_gather_into_tensor(gs, s.contiguous(), group=self.group)
+        dist.all_gather_into_tensor(gi, i.contiguous(), group=self.group)
+        return _ops.topk_merge(gs, gi, k)
+
+
+def merge_topk(scores, idx, k):
+    """[R, Q, k_in] per-shard lists -> [Q, k] by (score desc, index asc)."""
+    return _ops.topk_merge(scores, idx, k)

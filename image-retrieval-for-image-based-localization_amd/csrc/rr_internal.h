@@ -1,0 +1,87 @@
+// Internal helpers shared by the librr.so translation units (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/rr.h"
+
+namespace rr {
+
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Launch-error check: every entry point ends with this.
+inline int check_launch(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(RR_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+    return RR_OK;
+}
+
+// bf16 stored as raw uint16 bits.
+typedef uint16_t bf16_t;
+
+__device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+// round-to-nearest-even float -> bf16 (NaN kept NaN by the explicit branch).
+__device__ __host__ __forceinline__ bf16_t f2bf(float f) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t u = __float_as_uint(f);
+#else
+    uint32_t u;
+    __builtin_memcpy(&u, &f, 4);
+#endif
+    if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return (bf16_t)((u >> 16) | 0x40);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (bf16_t)(u >> 16);
+}
+
+template <typename T> struct DT;
+template <> struct DT<float> {
+    static __device__ __forceinline__ float load(const float* p) { return *p; }
+    static __device__ __forceinline__ float to_f(float v) { return v; }
+    static __device__ __forceinline__ float from_f(float v) { return v; }
+};
+template <> struct DT<bf16_t> {
+    static __device__ __forceinline__ float to_f(bf16_t v) { return bf2f(v); }
+    static __device__ __forceinline__ bf16_t from_f(float v) { return f2bf(v); }
+};
+
+// Arguments of the MFMA implicit-GEMM engine (rr_conv.hip); also drives the
+// kNN score GEMM (rr_knn.hip).
+struct ConvArgs {
+    const void* x;
+    const void* w;
+    const float* scale;
+    const float* shift;
+    const void* res;
+    void* y;
+    int n, h, w_, cin, ho, wo, cout, kh, kw, stride, pad, dil, kp, ldy, act, flags;
+    float slope;
+    int lc;  // log2(cin)
+    int P;   // n*ho*wo
+};
+// scores[p][c] (f32, row stride ldy) = x[p][:] . w[c][:], 1x1 GEMM, dtype in.
+void gemm_scores(const ConvArgs& a, int dtype, hipStream_t s);
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+}  // namespace rr

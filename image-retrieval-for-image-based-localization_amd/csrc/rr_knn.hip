@@ -1,0 +1,404 @@
+// librr.so — brute-force cosine kNN with exact ordering.
+//
+// Replaces `scores = np.dot(vecs.T, qvecs); ranks = np.argsort(-scores, 0)`
+// (scripts/test.py:247-248) restricted to the first k ranks.
+//
+// Pipeline per query batch (all on one HIP stream, no host sync):
+//  1. score GEMM   slab[q][n] = <q, db_n> for a pass of G chunks of L rows,
+//                  MFMA (bf16 or exact f32), f32 scores.  The slab is sized to
+//                  stay resident in the 256 MiB Infinity Cache (<= 64 MiB).
+//  2. chunk select per (query, chunk): radix-select of the top KC fp32 keys
+//                  over L scores staged in LDS; candidates emitted in index
+//                  order (deterministic, ties -> lower index).
+//  3. final        per query: radix-select top KC of all chunk candidates,
+//                  re-score them in float64 from the float32 rows (exact
+//                  products, fixed-order reduction), bitonic sort by
+//                  (score desc, index asc), emit k.
+// KC > k is the screening margin: bf16 scores err by ~1e-4, exact-f32 by
+// ~1e-7, far below KC-k candidates' worth of score density at the boundary.
+#include "rr_internal.h"
+
+namespace rr {
+
+
+constexpr int SEL_THREADS = 1024;
+constexpr int SEL_WAVES = SEL_THREADS / 64;
+constexpr int CHUNK_L = 16384;           // rows per select chunk (keys staged in 64 KiB LDS)
+constexpr size_t SLAB_BUDGET = 64ull << 20;
+constexpr int MAX_SORT = 8192;
+
+__device__ __forceinline__ uint32_t fkey(float f) {
+    uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float funkey(uint32_t k) {
+    return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+// Block-wide exclusive scan of one int per thread (SEL_THREADS threads).
+__device__ __forceinline__ int block_excl_scan(int v, int* wsum, int& total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    if (w == 0) {
+        int t = lane < SEL_WAVES ? wsum[lane] : 0;
+        int s = t;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            int y = __shfl_up(s, o, 64);
+            if (lane >= o) s += y;
+        }
+        if (lane < SEL_WAVES) wsum[lane] = s - t;
+        if (lane == SEL_WAVES - 1) wsum[SEL_WAVES] = s;
+    }
+    __syncthreads();
+    int res = wsum[w] + x - v;
+    total = wsum[SEL_WAVES];
+    __syncthreads();
+    return res;
+}
+
+// Top-K (largest keys) of keys[0..len) with index-order ties.  `getk(i)` gives
+// the key, `geti(i)` the payload index; K results are written to out_k/out_i
+// in ascending position order; missing slots get (key 0, index -1).
+template <typename GK, typename GI>
+__device__ void block_topk(GK getk, GI geti, int len, int K, uint32_t* out_k, int* out_i, int* smem_i) {
+    int* hist = smem_i;             // 256
+    int* wsum = smem_i + 256;       // SEL_WAVES + 1
+    int* sel = smem_i + 256 + 32;   // [0]=digit, [1]=remaining
+    const int tid = threadIdx.x;
+    uint32_t thr = 0;
+    int remaining = K;
+    if (len > K) {
+        uint32_t prefix = 0, mask = 0;
+        for (int shift = 24; shift >= 0; shift -= 8) {
+            for (int i = tid; i < 256; i += SEL_THREADS) hist[i] = 0;
+            __syncthreads();
+            for (int i = tid; i < len; i += SEL_THREADS) {
+                uint32_t k = getk(i);
+                if ((k & mask) == prefix) atomicAdd(&hist[(k >> shift) & 255], 1);
+            }
+            __syncthreads();
+            if (tid < 64) {
+                // wave 0: suffix sums over 256 bins (4 per lane), find the digit
+                int c0 = hist[tid * 4 + 0], c1 = hist[tid * 4 + 1], c2 = hist[tid * 4 + 2], c3 = hist[tid * 4 + 3];
+                int lsum = c0 + c1 + c2 + c3;
+                // inclusive suffix scan across lanes (lane 63 holds the highest digits)
+                int s = lsum;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    int y = __shfl_down(s, o, 64);
+                    if (tid + o < 64) s += y;
+                }
+                int above = s - lsum;  // count of keys with digit > 4*tid+3
+                // within lane: digits 4*tid+3 .. 4*tid
+                int cs[4] = {c0, c1, c2, c3};
+                int acc = above;
+                for (int d = 3; d >= 0; --d) {
+                    if (acc < remaining && acc + cs[d] >= remaining) {
+                        sel[0] = tid * 4 + d;
+                        sel[1] = remaining - acc;
+                    }
+                    acc += cs[d];
+                }
+            }
+            __syncthreads();
+            const int digit = sel[0];
+            remaining = sel[1];
+            prefix |= (uint32_t)digit << shift;
+            mask |= 255u << shift;
+            __syncthreads();
+        }
+        thr = prefix;
+    }
+    // ordered emission: thread t owns the contiguous segment [t*seg, (t+1)*seg)
+    const int seg = (len + SEL_THREADS - 1) / SEL_THREADS;
+    const int b = tid * seg, e = min(len, b + seg);
+    int ngt = 0, neq = 0;
+    if (len > K) {
+        for (int i = b; i < e; ++i) {
+            uint32_t k = getk(i);
+            ngt += k > thr;
+            neq += k == thr;
+        }
+    } else {
+        ngt = max(0, e - b);
+    }
+    int tot_gt, tot_eq;
+    int pgt = block_excl_scan(ngt, wsum, tot_gt);
+    int peq = block_excl_scan(neq, wsum, tot_eq);
+    // gt items occupy [0, tot_gt) in position order; then the first
+    // `remaining` eq items.  Merge both in position order: an item's slot is
+    // (#gt before it) + (#taken eq before it).
+    if (len > K) {
+        int gi = pgt, ei = peq;
+        for (int i = b; i < e; ++i) {
+            uint32_t k = getk(i);
+            if (k > thr) {
+                int slot = gi + min(ei, remaining);
+                out_k[slot] = k;
+                out_i[slot] = geti(i);
+                ++gi;
+            } else if (k == thr) {
+                if (ei < remaining) {
+                    int slot = gi + ei;
+                    out_k[slot] = k;
+                    out_i[slot] = geti(i);
+                }
+                ++ei;
+            }
+        }
+    } else {
+        for (int i = b; i < e; ++i) {
+            out_k[pgt + i - b] = getk(i);
+            out_i[pgt + i - b] = geti(i);
+        }
+        for (int i = len + tid; i < K; i += SEL_THREADS) {
+            out_k[i] = 0u;
+            out_i[i] = -1;
+        }
+    }
+    __syncthreads();
+}
+
+// ---------------------------------------------------------------- chunk select
+// grid (nq, chunks in pass).  slab row q: slab + q*S; chunk c covers
+// columns [c*L, c*L + len).  Global row index of column j = row0 + c*L + j.
+__global__ void __launch_bounds__(SEL_THREADS) k_chunk_select(const float* __restrict__ slab, long long S, int L,
+                                                              int rows_in_pass, int row0, int chunk0, int nchunks,
+                                                              int KC, uint32_t* __restrict__ cand_k,
+                                                              int* __restrict__ cand_i) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t keys[];  // L
+    __shared__ int smi[256 + 64];
+    const int q = blockIdx.x, c = blockIdx.y;
+    const int len = min(L, rows_in_pass - c * L);
+    const float* src = slab + (long long)q * S + (long long)c * L;
+    for (int i = threadIdx.x; i < len; i += SEL_THREADS) keys[i] = fkey(src[i]);
+    __syncthreads();
+    const long long o = ((long long)q * nchunks + chunk0 + c) * KC;
+    const int base = row0 + c * L;
+    block_topk([&](int i) { return keys[i]; }, [&](int i) { return base + i; }, len, KC, cand_k + o, cand_i + o, smi);
+}
+
+// ------------------------------------------------------------------ bitonic
+// Struct-of-arrays sort of (score f64, index) pairs, best first:
+// better(a, b) = a.s > b.s || (a.s == b.s && a.i < b.i).  Sentinel: (-inf, MAX).
+template <typename I>
+__device__ __forceinline__ bool better(double sa, I ia, double sb, I ib) {
+    return sa > sb || (sa == sb && ia < ib);
+}
+template <typename I>
+__device__ void bitonic_best_first(double* ks, I* is, int n) {
+    for (int k = 2; k <= n; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int t = threadIdx.x; t < n; t += blockDim.x) {
+                int p = t ^ j;
+                if (p > t) {
+                    bool up = (t & k) == 0;
+                    double sa = ks[t], sb = ks[p];
+                    I ia = is[t], ib = is[p];
+                    if (up ? better(sb, ib, sa, ia) : better(sa, ia, sb, ib)) {
+                        ks[t] = sb; ks[p] = sa;
+                        is[t] = ib; is[p] = ia;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// ------------------------------------------------------------------ final
+// grid (nq).  Dynamic LDS: double ks[npow2] | int is[npow2] | u32 sk[KC] | int si[KC].
+__global__ void __launch_bounds__(SEL_THREADS) k_final(const uint32_t* __restrict__ cand_k, const int* __restrict__ cand_i,
+                                                       int ncand, int KC, int npow2, const float* __restrict__ db32,
+                                                       const float* __restrict__ q32, int d, int k,
+                                                       long long idx_offset, double* __restrict__ out_s,
+                                                       long long* __restrict__ out_i) {
+    extern __shared__ __attribute__((aligned(16))) char dyn[];
+    double* ks = reinterpret_cast<double*>(dyn);
+    int* is = reinterpret_cast<int*>(ks + npow2);
+    uint32_t* sk = reinterpret_cast<uint32_t*>(is + npow2);
+    int* si = reinterpret_cast<int*>(sk + KC);
+    __shared__ int smi[256 + 64];
+    const int q = blockIdx.x;
+    const uint32_t* ck = cand_k + (long long)q * ncand;
+    const int* ci = cand_i + (long long)q * ncand;
+    // sentinel candidates (index -1) carry key 0 = below every real score key
+    block_topk([&](int i) { return ck[i]; }, [&](int i) { return ci[i]; }, ncand, KC, sk, si, smi);
+    // float64 re-score: one wave per candidate, lane-strided products in a
+    // fixed order, butterfly reduction -> bit-reproducible on any sharding.
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const float* qr = q32 + (long long)q * d;
+    for (int j = w; j < npow2; j += SEL_WAVES) {
+        const int idx = j < KC ? si[j] : -1;
+        double sc = -INFINITY;
+        if (idx >= 0) {
+            const float* dr = db32 + (long long)idx * d;
+            double acc = 0.0;
+            for (int t = lane; t < d; t += 64) acc = fma((double)dr[t], (double)qr[t], acc);
+            sc = wave_sum_d(acc);
+        }
+        if (lane == 0) {
+            ks[j] = sc;
+            is[j] = idx >= 0 ? idx : 0x7fffffff;
+        }
+    }
+    __syncthreads();
+    bitonic_best_first(ks, is, npow2);
+    for (int j = threadIdx.x; j < k; j += SEL_THREADS) {
+        const int i = is[j];
+        out_s[(long long)q * k + j] = ks[j];
+        out_i[(long long)q * k + j] = i == 0x7fffffff ? -1 : (long long)i + idx_offset;
+    }
+}
+
+// ------------------------------------------------------------------ merge
+__global__ void __launch_bounds__(SEL_THREADS) k_merge(const double* __restrict__ in_s, const long long* __restrict__ in_i,
+                                                       int r, int nq, int k_in, int k, int npow2,
+                                                       double* __restrict__ out_s, long long* __restrict__ out_i) {
+    extern __shared__ __attribute__((aligned(16))) char dyn[];
+    double* ks = reinterpret_cast<double*>(dyn);
+    long long* is = reinterpret_cast<long long*>(ks + npow2);
+    const long long SENT = 0x7fffffffffffffffll;
+    const int q = blockIdx.x;
+    const int n = r * k_in;
+    for (int j = threadIdx.x; j < npow2; j += SEL_THREADS) {
+        double sc = -INFINITY;
+        long long id = SENT;
+        if (j < n) {
+            const int src = j / k_in, jj = j - src * k_in;
+            const long long o = ((long long)src * nq + q) * k_in + jj;
+            if (in_i[o] >= 0) { sc = in_s[o]; id = in_i[o]; }
+        }
+        ks[j] = sc;
+        is[j] = id;
+    }
+    __syncthreads();
+    bitonic_best_first(ks, is, npow2);
+    for (int j = threadIdx.x; j < k; j += SEL_THREADS) {
+        out_s[(long long)q * k + j] = ks[j];
+        out_i[(long long)q * k + j] = is[j] == SENT ? -1 : is[j];
+    }
+}
+
+static int pow2_at_least(int v) {
+    int p = 1;
+    while (p < v) p <<= 1;
+    return p;
+}
+
+struct KnnPlan {
+    int L, nchunks, G, KC, npow2;
+    long long S;
+    size_t slab_bytes, cand_bytes, total;
+};
+
+static int default_cand(int k, int dtype) {
+    int extra = dtype == RR_BF16 ? 128 : 32;
+    return ((k + extra + 63) / 64) * 64;
+}
+
+static KnnPlan plan(long long n_db, int nq, int k, int cand, int dtype) {
+    KnnPlan p;
+    p.KC = cand > 0 ? cand : default_cand(k, dtype);
+    p.L = (int)(n_db < CHUNK_L ? n_db : CHUNK_L);
+    p.nchunks = (int)((n_db + p.L - 1) / p.L);
+    long long g = (long long)(SLAB_BUDGET / ((size_t)nq * p.L * 4));
+    if (g < 1) g = 1;
+    if (g > p.nchunks) g = p.nchunks;
+    if (g * p.L > (4ll << 20)) g = (4ll << 20) / p.L;  // <= 4M rows per GEMM pass (grid.y limit)
+    if (g < 1) g = 1;
+    p.G = (int)g;
+    p.S = ((long long)p.G * p.L + 3) / 4 * 4;
+    p.npow2 = pow2_at_least(p.KC);
+    p.slab_bytes = ((size_t)nq * p.S * 4 + 255) / 256 * 256;
+    p.cand_bytes = (size_t)nq * p.nchunks * p.KC * 4;
+    p.total = p.slab_bytes + 2 * ((p.cand_bytes + 255) / 256 * 256);
+    return p;
+}
+
+}  // namespace rr
+
+using namespace rr;
+
+extern "C" {
+
+size_t rr_knn_workspace_bytes(long long n_db, int nq, int d, int k, int cand, int dtype) {
+    (void)d;
+    if (n_db <= 0 || nq <= 0) return 0;
+    return plan(n_db, nq, k, cand, dtype).total;
+}
+
+int rr_knn_topk(const void* db, const float* db_f32, long long n_db, const void* q, const float* q_f32, int nq, int d,
+                int k, int cand, long long idx_offset, double* out_scores, long long* out_idx, void* workspace,
+                size_t workspace_bytes, int dtype, void* stream) {
+    if (n_db <= 0 || nq <= 0 || k <= 0) return fail(RR_EINVAL, "rr_knn_topk: empty problem");
+    if (n_db > 0x7fffffffll) return fail(RR_EINVAL, "rr_knn_topk: shard rows must fit int32 (shard the database)");
+    if (dtype != RR_BF16 && dtype != RR_F32) return fail(RR_EINVAL, "rr_knn_topk: dtype");
+    if (d <= 0 || d % 32 || (d & (d - 1))) return fail(RR_EINVAL, "rr_knn_topk: d must be a power of two >= 32");
+    KnnPlan p = plan(n_db, nq, k, cand, dtype);
+    if (p.KC < k) return fail(RR_EINVAL, "rr_knn_topk: cand must be >= k");
+    if (p.npow2 > MAX_SORT) return fail(RR_EINVAL, "rr_knn_topk: k / cand too large (max 8192)");
+    if (workspace_bytes < p.total || !workspace) return fail(RR_ENOSPACE, "rr_knn_topk: workspace too small");
+    hipStream_t s = as_stream(stream);
+    char* ws = (char*)workspace;
+    float* slab = (float*)ws;
+    uint32_t* cand_k = (uint32_t*)(ws + p.slab_bytes);
+    int* cand_i = (int*)(ws + p.slab_bytes + (p.cand_bytes + 255) / 256 * 256);
+
+    static bool attr_done = false;
+    if (!attr_done) {
+        (void)hipFuncSetAttribute((const void*)k_chunk_select, hipFuncAttributeMaxDynamicSharedMemorySize, CHUNK_L * 4);
+        (void)hipFuncSetAttribute((const void*)k_final, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 4096);
+        (void)hipFuncSetAttribute((const void*)k_merge, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 4096);
+        attr_done = true;
+    }
+
+    const size_t esz = dtype == RR_BF16 ? 2 : 4;
+    for (long long r0 = 0; r0 < n_db; r0 += (long long)p.G * p.L) {
+        const int rows = (int)((n_db - r0) < (long long)p.G * p.L ? (n_db - r0) : (long long)p.G * p.L);
+        ConvArgs a{};
+        a.x = q;
+        a.w = (const char*)db + (size_t)r0 * d * esz;
+        a.y = slab;
+        a.n = 1; a.h = 1; a.w_ = nq; a.cin = d; a.ho = 1; a.wo = nq; a.cout = rows;
+        a.kh = 1; a.kw = 1; a.stride = 1; a.pad = 0; a.dil = 1; a.kp = d; a.ldy = (int)p.S;
+        a.act = RR_ACT_IDENTITY; a.flags = 0; a.slope = 0.f;
+        a.lc = __builtin_ctz((unsigned)d);
+        a.P = nq;
+        gemm_scores(a, dtype, s);
+        const int chunks = (rows + p.L - 1) / p.L;
+        hipLaunchKernelGGL(k_chunk_select, dim3(nq, chunks), dim3(SEL_THREADS), (size_t)p.L * 4, s, slab, p.S, p.L,
+                           rows, (int)r0, (int)(r0 / p.L), p.nchunks, p.KC, cand_k, cand_i);
+    }
+    const size_t fin_lds = (size_t)p.npow2 * 12 + (size_t)p.KC * 8;
+    if (fin_lds > 160 * 1024 - 4096) return fail(RR_EINVAL, "rr_knn_topk: candidate set exceeds LDS");
+    hipLaunchKernelGGL(k_final, dim3(nq), dim3(SEL_THREADS), fin_lds, s, cand_k, cand_i, p.nchunks * p.KC, p.KC,
+                       p.npow2, db_f32, q_f32, d, k, idx_offset, out_scores, out_idx);
+    return check_launch("rr_knn_topk");
+}
+
+int rr_topk_merge(const double* in_scores, const long long* in_idx, int r, int nq, int k_in, int k, double* out_scores,
+                  long long* out_idx, void* stream) {
+    if (r <= 0 || nq <= 0 || k_in <= 0 || k <= 0) return fail(RR_EINVAL, "rr_topk_merge: empty");
+    const int n = r * k_in;
+    const int np2 = pow2_at_least(n < k ? k : n);
+    if (np2 > MAX_SORT) return fail(RR_EINVAL, "rr_topk_merge: r*k_in too large");
+    static bool attr_done = false;
+    if (!attr_done) {
+        (void)hipFuncSetAttribute((const void*)k_merge, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 4096);
+        attr_done = true;
+    }
+    hipLaunchKernelGGL(k_merge, dim3(nq), dim3(SEL_THREADS), (size_t)np2 * 16, as_stream(stream),
+                       in_scores, in_idx, r, nq, k_in, k, np2, out_scores, out_idx);
+    return check_launch("rr_topk_merge");
+}
+
+}  // extern "C"

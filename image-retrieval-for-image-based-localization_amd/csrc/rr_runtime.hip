@@ -1,0 +1,239 @@
+// librr.so — runtime helpers and the small memory-bound extractor ops:
+// error state, image normalise + NCHW->NHWC, max-pool, bilinear resize,
+// synthetic-row generator, f32->bf16 cast.  gfx950 only.
+#include "rr_internal.h"
+
+#include <cstring>
+
+namespace rr {
+
+static thread_local std::string g_err;
+
+void set_error(const std::string& msg) { g_err = msg; }
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+// ------------------------------------------------------------------ normalise
+struct NormParams {
+    float mean[4];
+    float stdv[4];
+};
+
+// One thread per output pixel: reads c planes (coalesced along w), writes c_pad
+// contiguous channels (16 B for bf16 x 8 / f32 x 4).  (x - mean) / std is
+// evaluated as in cirtorch/utils/image.py:125 ((x - m) / s, true division).
+template <typename T>
+__global__ void k_image_to_nhwc(const float* __restrict__ src, int n, int c, int hw, NormParams np,
+                                int do_norm, T* __restrict__ dst, int c_pad) {
+    long long pix = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    long long total = (long long)n * hw;
+    if (pix >= total) return;
+    long long img = pix / hw;
+    long long off = pix - img * hw;
+    const float* s = src + img * c * hw + off;
+    T* d = dst + pix * c_pad;
+    for (int ch = 0; ch < c_pad; ++ch) {
+        float v = 0.f;
+        if (ch < c) {
+            v = s[(long long)ch * hw];
+            if (do_norm) v = (v - np.mean[ch]) / np.stdv[ch];
+        }
+        d[ch] = DT<T>::from_f(v);
+    }
+}
+
+// ------------------------------------------------------------------ max-pool
+template <typename T>
+__global__ void k_maxpool_nhwc(const T* __restrict__ x, int n, int h, int w, int c, int k, int stride,
+                               int pad, T* __restrict__ y, int ho, int wo) {
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    long long total = (long long)n * ho * wo * c;
+    if (i >= total) return;
+    int ch = (int)(i % c);
+    long long r = i / c;
+    int ow = (int)(r % wo);
+    r /= wo;
+    int oh = (int)(r % ho);
+    int img = (int)(r / ho);
+    float m = -INFINITY;
+    int h0 = oh * stride - pad, w0 = ow * stride - pad;
+    for (int a = 0; a < k; ++a) {
+        int hh = h0 + a;
+        if (hh < 0 || hh >= h) continue;
+        for (int b = 0; b < k; ++b) {
+            int ww = w0 + b;
+            if (ww < 0 || ww >= w) continue;
+            m = fmaxf(m, DT<T>::to_f(x[(((long long)img * h + hh) * w + ww) * c + ch]));
+        }
+    }
+    y[i] = DT<T>::from_f(m);
+}
+
+// ------------------------------------------------------------ bilinear resize
+// align_corners=False source index, as torch's area_pixel_compute_source_index
+// for linear modes: src = scale*(dst+0.5)-0.5 clamped at 0.
+__global__ void k_resize_bilinear(const float* __restrict__ src, int c, int h, int w, float* __restrict__ dst,
+                                  int ho, int wo, float sh, float sw) {
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    long long total = (long long)c * ho * wo;
+    if (i >= total) return;
+    int ox = (int)(i % wo);
+    long long r = i / wo;
+    int oy = (int)(r % ho);
+    int ch = (int)(r / ho);
+    float fy = fmaxf(sh * (oy + 0.5f) - 0.5f, 0.f);
+    float fx = fmaxf(sw * (ox + 0.5f) - 0.5f, 0.f);
+    int y0 = (int)fy, x0 = (int)fx;
+    int y1 = y0 + (y0 < h - 1 ? 1 : 0);
+    int x1 = x0 + (x0 < w - 1 ? 1 : 0);
+    float ly1 = fy - y0, ly0 = 1.f - ly1;
+    float lx1 = fx - x0, lx0 = 1.f - lx1;
+    const float* p = src + (long long)ch * h * w;
+    float v = ly0 * (lx0 * p[(long long)y0 * w + x0] + lx1 * p[(long long)y0 * w + x1]) +
+              ly1 * (lx0 * p[(long long)y1 * w + x0] + lx1 * p[(long long)y1 * w + x1]);
+    dst[i] = v;
+}
+
+// ------------------------------------------------------------ synthetic rows
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// One block (256 threads) per row; Box-Muller on 2 x 24-bit uniforms per pair.
+__global__ void __launch_bounds__(256) k_fill_unit_rows(float* __restrict__ out, int d, uint64_t seed,
+                                                        long long row0) {
+    long long row = blockIdx.x;
+    uint64_t base = splitmix64(seed ^ (uint64_t)(row0 + row) * 0xD1B54A32D192ED03ull);
+    __shared__ double red[4];
+    float vals[16];
+    double ss = 0.0;
+    int per = (d + 255) / 256;  // <= 16 (d <= 4096)
+    for (int t = 0; t < per; t += 2) {
+        int j = (threadIdx.x + 256 * t);
+        uint64_t h = splitmix64(base + (uint64_t)j);
+        float u1 = ((h >> 40) + 1) * (1.0f / 16777217.0f);
+        float u2 = ((h >> 16) & 0xFFFFFF) * (1.0f / 16777216.0f);
+        float r = sqrtf(-2.f * logf(u1));
+        float s, c;
+        sincosf(6.28318530717958647f * u2, &s, &c);
+        vals[t] = r * c;
+        if (t + 1 < per) vals[t + 1] = r * s;
+    }
+    for (int t = 0; t < per; ++t) {
+        int j = threadIdx.x + 256 * t;
+        if (j < d) ss += (double)vals[t] * vals[t];
+    }
+    ss = wave_sum_d(ss);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+    __syncthreads();
+    double tot = red[0] + red[1] + red[2] + red[3];
+    float inv = (float)(1.0 / sqrt(tot));
+    for (int t = 0; t < per; ++t) {
+        int j = threadIdx.x + 256 * t;
+        if (j < d) out[row * d + j] = vals[t] * inv;
+    }
+}
+
+__global__ void k_cast_f32_bf16(const float* __restrict__ x, bf16_t* __restrict__ y, long long n) {
+    long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    if (i + 3 < n) {
+        float4 v = *reinterpret_cast<const float4*>(x + i);
+        ushort4 o;
+        o.x = f2bf(v.x); o.y = f2bf(v.y); o.z = f2bf(v.z); o.w = f2bf(v.w);
+        *reinterpret_cast<ushort4*>(y + i) = o;
+    } else {
+        for (; i < n; ++i) y[i] = f2bf(x[i]);
+    }
+}
+
+static inline unsigned nblk(long long total, int b) { return (unsigned)((total + b - 1) / b); }
+
+}  // namespace rr
+
+using namespace rr;
+
+extern "C" {
+
+int rr_version(void) { return 1; }
+
+const char* rr_last_error(void) { return g_err.c_str(); }
+
+int rr_device_arch(char* buf, int buflen) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return fail(RR_EHIP, "hipGetDevice failed");
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return fail(RR_EHIP, "hipGetDeviceProperties failed");
+    std::strncpy(buf, prop.gcnArchName, buflen - 1);
+    buf[buflen - 1] = 0;
+    return RR_OK;
+}
+
+int rr_image_to_nhwc(const float* src, int n, int c, int h, int w, const float* mean_host,
+                     const float* std_host, int do_normalize, void* dst, int c_pad, int dtype,
+                     void* stream) {
+    if (c > 4 || c_pad < c || n <= 0 || h <= 0 || w <= 0) return fail(RR_EINVAL, "rr_image_to_nhwc: bad shape");
+    NormParams np{};
+    for (int i = 0; i < c; ++i) {
+        np.mean[i] = do_normalize ? mean_host[i] : 0.f;
+        np.stdv[i] = do_normalize ? std_host[i] : 1.f;  // divisor (true division in kernel)
+    }
+    long long total = (long long)n * h * w;
+    if (dtype == RR_BF16)
+        hipLaunchKernelGGL(k_image_to_nhwc<bf16_t>, dim3(nblk(total, 256)), dim3(256), 0, as_stream(stream), src, n,
+                           c, h * w, np, do_normalize, (bf16_t*)dst, c_pad);
+    else if (dtype == RR_F32)
+        hipLaunchKernelGGL(k_image_to_nhwc<float>, dim3(nblk(total, 256)), dim3(256), 0, as_stream(stream), src, n, c,
+                           h * w, np, do_normalize, (float*)dst, c_pad);
+    else
+        return fail(RR_EINVAL, "rr_image_to_nhwc: dtype");
+    return check_launch("rr_image_to_nhwc");
+}
+
+int rr_maxpool2d(const void* x, int n, int h, int w, int c, int k, int stride, int pad, void* y, int ho, int wo,
+                 int dtype, void* stream) {
+    long long total = (long long)n * ho * wo * c;
+    if (total <= 0) return fail(RR_EINVAL, "rr_maxpool2d: empty");
+    if (dtype == RR_BF16)
+        hipLaunchKernelGGL(k_maxpool_nhwc<bf16_t>, dim3(nblk(total, 256)), dim3(256), 0, as_stream(stream),
+                           (const bf16_t*)x, n, h, w, c, k, stride, pad, (bf16_t*)y, ho, wo);
+    else if (dtype == RR_F32)
+        hipLaunchKernelGGL(k_maxpool_nhwc<float>, dim3(nblk(total, 256)), dim3(256), 0, as_stream(stream),
+                           (const float*)x, n, h, w, c, k, stride, pad, (float*)y, ho, wo);
+    else
+        return fail(RR_EINVAL, "rr_maxpool2d: dtype");
+    return check_launch("rr_maxpool2d");
+}
+
+int rr_resize_bilinear(const float* src, int c, int h, int w, float* dst, int ho, int wo, double scale_h,
+                       double scale_w, void* stream) {
+    long long total = (long long)c * ho * wo;
+    if (total <= 0) return fail(RR_EINVAL, "rr_resize_bilinear: empty");
+    hipLaunchKernelGGL(k_resize_bilinear, dim3(nblk(total, 256)), dim3(256), 0, as_stream(stream), src, c, h, w, dst,
+                       ho, wo, (float)scale_h, (float)scale_w);
+    return check_launch("rr_resize_bilinear");
+}
+
+int rr_fill_unit_rows(float* out, long long rows, int d, unsigned long long seed, long long row0, void* stream) {
+    if (d <= 0 || d > 4096 || rows <= 0) return fail(RR_EINVAL, "rr_fill_unit_rows: d must be in (0, 4096]");
+    const long long maxgrid = 1ll << 30;
+    for (long long r = 0; r < rows; r += maxgrid) {
+        long long cnt = rows - r < maxgrid ? rows - r : maxgrid;
+        hipLaunchKernelGGL(k_fill_unit_rows, dim3((unsigned)cnt), dim3(256), 0, as_stream(stream), out + r * d, d,
+                           (uint64_t)seed, row0 + r);
+    }
+    return check_launch("rr_fill_unit_rows");
+}
+
+int rr_cast_f32_bf16(const float* x, void* y, long long n, void* stream) {
+    if (n <= 0) return RR_OK;
+    hipLaunchKernelGGL(k_cast_f32_bf16, dim3(nblk((n + 3) / 4, 256)), dim3(256), 0, as_stream(stream), x,
+                       (bf16_t*)y, n);
+    return check_launch("rr_cast_f32_bf16");
+}
+
+}  // extern "C"

@@ -1,0 +1,155 @@
+/*
+ * rr.h — C ABI of librr.so, the MI355X (gfx950) extract-and-match engine.
+ *
+ * The reference (Tarekbouamer/Image-Retrieval-for-Image-Based-Localization,
+ * package `cirtorch`) is pure Python: its hot path is a chain of torch
+ * nn.Modules plus two numpy calls.  Each entry point below replaces one
+ * reference operator; the Python host package `cirtorch` (same module names,
+ * same argument meaning) binds them with ctypes — see INTEGRATION.md.
+ *
+ * Conventions
+ *   - every function returns 0 on success, a negative code on error;
+ *     rr_last_error() returns the message (thread-local).
+ *   - all tensor pointers are DEVICE pointers; nothing here allocates:
+ *     scratch is caller-provided and sized by the matching *_workspace_bytes.
+ *   - `stream` is a hipStream_t (NULL = default stream); every call only
+ *     enqueues work (no host synchronisation), so calls are graph-capturable.
+ *   - activations are NHWC ("channels_last"); dtype codes below.
+ *   - re-entrant; one process per GPU.
+ */
+#ifndef RR_H_
+#define RR_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum rr_dtype { RR_F32 = 0, RR_BF16 = 1 };
+enum rr_act { RR_ACT_IDENTITY = 0, RR_ACT_LEAKY = 1 };
+enum rr_pool_mode { RR_POOL_GEM = 0, RR_POOL_MAC = 1, RR_POOL_SPOC = 2 };
+enum rr_conv_flags { RR_CONV_AFFINE = 1, RR_CONV_RESIDUAL = 2 };
+enum rr_layout { RR_NHWC = 0, RR_NCHW = 1 };
+
+#define RR_OK 0
+#define RR_EINVAL -1
+#define RR_EHIP -2
+#define RR_ENOSPACE -3
+
+/* ------------------------------------------------------------------ runtime */
+int rr_version(void);
+const char* rr_last_error(void);
+/* Device architecture name of the current device (e.g. "gfx950"). */
+int rr_device_arch(char* buf, int buflen);
+
+/* ------------------------------------------------------------ extractor ops */
+
+/* NCHW float32 image batch -> NHWC `dtype` with `c_pad` channels (zeros in the
+ * pad channels), optionally (x - mean_c) / std_c.
+ * Replaces cirtorch/utils/image.py:86-127 `normalize` (called from
+ * datasets/augmentation/random_augmentation.py:174) fused with the layout
+ * change the conv stack needs.  mean/std are HOST arrays of c floats. */
+int rr_image_to_nhwc(const float* src, int n, int c, int h, int w,
+                     const float* mean_host, const float* std_host, int do_normalize,
+                     void* dst, int c_pad, int dtype, void* stream);
+
+/* Implicit-GEMM convolution on MFMA with a fused epilogue:
+ *   y = act( conv(x, w) * scale[c] + shift[c] (+ residual) )
+ * Replaces nn.Conv2d (cirtorch/backbones/resnet.py:61, backbones/misc.py:166-180)
+ * followed by the inplace_abn ABN eval BN + leaky_relu / identity
+ * (utils/misc.py:175-235) and the residual add + activation of
+ * ResidualBlock.forward (backbones/misc.py:184-203).
+ *   x  : [n][h][w][c_in]            (dtype)
+ *   w  : [c_out][k_packed]          (dtype) k = (kh*KW + kw)*c_in + ci, zero padded
+ *   y  : [n*ho*wo][ldy]             (out_dtype), channel c at column c
+ *   residual : same layout/dtype as y (flag RR_CONV_RESIDUAL)
+ * Also used as the score GEMM of the kNN (1x1, ldy = slab width). */
+typedef struct rr_conv_desc {
+    int n, h, w, c_in;     /* input; c_in = channel stride, power of two */
+    int ho, wo, c_out;     /* output */
+    int kh, kw, stride, pad, dil;
+    int k_packed;          /* weight row length, multiple of 32 */
+    int ldy;               /* output row stride in elements (>= c_out) */
+    int act;               /* rr_act */
+    float slope;           /* leaky slope */
+    int flags;             /* rr_conv_flags */
+} rr_conv_desc;
+
+int rr_conv2d_fused(const void* x, const void* w, const float* scale, const float* shift,
+                    const void* residual, void* y, const rr_conv_desc* desc,
+                    int dtype, int out_dtype, void* stream);
+
+/* 3x3/s2/p1 style max pooling, NHWC.  Replaces nn.MaxPool2d(3, stride=2,
+ * padding=1) of the stem (cirtorch/backbones/resnet.py:65). */
+int rr_maxpool2d(const void* x, int n, int h, int w, int c, int k, int stride, int pad,
+                 void* y, int ho, int wo, int dtype, void* stream);
+
+/* Bilinear resize, align_corners=False, NCHW float32 (one image).
+ * Replaces nn.functional.interpolate(scale_factor=s, mode='bilinear',
+ * align_corners=False) of the multi-scale pyramid (cirtorch/models/GF_net.py:32-35). */
+int rr_resize_bilinear(const float* src, int c, int h, int w, float* dst, int ho, int wo,
+                       double scale_h, double scale_w, void* stream);
+
+/* Global pooling to out[n][c] float32.
+ * GeM: (mean_hw max(x,eps)^p)^(1/p)  — cirtorch/modules/pools.py:30-38
+ * MAC: max_hw x                      — pools.py:10-16
+ * SPoC: mean_hw x                    — pools.py:20-26
+ * x layout RR_NHWC ([n][hw][c], any dtype) or RR_NCHW ([n][c][hw]). */
+int rr_global_pool(const void* x, int n, int c, int hw, int layout, int mode,
+                   float p, float eps, float* out, int dtype, void* stream);
+
+/* Row L2 normalisation y = x / (||x||_2 + eps) over `dim` contiguous floats.
+ * Replaces cirtorch/modules/normalizations.py:9-16 (L2N). In-place allowed. */
+int rr_l2n_rows(const float* x, int rows, int dim, float eps, float* y, void* stream);
+
+/* Dense layer y[r][o] = sum_i x[r][i] * W[o][i] + b[o] (b may be NULL), fp32.
+ * Replaces the nn.Linear "learned whitening" of globalHead
+ * (cirtorch/modules/heads/global_head.py:26,63). */
+int rr_linear_rows(const float* x, int rows, int in_dim, const float* w, const float* b,
+                   int out_dim, float* y, void* stream);
+
+/* Fused globalHead tail: y = L2N(W . L2N(x) + b) (whiten != 0) or L2N(x).
+ * x: pooled [rows][dim] f32.  Replaces global_head.py:52-67 after the pool.
+ * workspace: rr_head_workspace_bytes(rows, dim). */
+size_t rr_head_workspace_bytes(int rows, int dim);
+int rr_head_l2n_whiten_l2n(const float* x, int rows, int dim, const float* w, const float* b,
+                           int whiten, float eps, float* y, void* workspace, void* stream);
+
+/* --------------------------------------------------------------- matching */
+
+/* Brute-force cosine kNN with exact ordering.
+ * Replaces `scores = np.dot(vecs.T, qvecs); ranks = np.argsort(-scores, axis=0)`
+ * (scripts/test.py:247-248, scripts/train_globalF.py:733-734), returning only
+ * the first k ranks.  Candidates are screened with an MFMA score GEMM in
+ * `dtype` (db/q), then re-scored in float64 from the float32 copies and
+ * ordered by (score desc, index asc).
+ *   db      : [n_db][d] (dtype)      db_f32 : [n_db][d] float32 (re-rank)
+ *   q       : [nq][d]   (dtype)      q_f32  : [nq][d]   float32
+ *   out_scores : [nq][k] float64     out_idx : [nq][k] int64 (+ idx_offset)
+ * `cand` = candidates kept per query (>= k); 0 picks the default for dtype. */
+size_t rr_knn_workspace_bytes(long long n_db, int nq, int d, int k, int cand, int dtype);
+int rr_knn_topk(const void* db, const float* db_f32, long long n_db,
+                const void* q, const float* q_f32, int nq, int d, int k, int cand,
+                long long idx_offset, double* out_scores, long long* out_idx,
+                void* workspace, size_t workspace_bytes, int dtype, void* stream);
+
+/* Merge R per-shard top-k lists per query into one top-k by (score desc,
+ * index asc).  in_*: [R][nq][k_in]; out_*: [nq][k].  Used after the RCCL
+ * all-gather of per-shard results.  k_in*R <= 4096. */
+int rr_topk_merge(const double* in_scores, const long long* in_idx, int r, int nq, int k_in,
+                  int k, double* out_scores, long long* out_idx, void* stream);
+
+/* ----------------------------------------------------------- data helpers */
+/* Counter-based N(0,1) rows, each L2-normalised: row i of the global matrix
+ * depends only on (seed, i0 + i), so shards generate identical rows. */
+int rr_fill_unit_rows(float* out, long long rows, int d, unsigned long long seed,
+                      long long row0, void* stream);
+/* float32 -> bf16 (round to nearest even). */
+int rr_cast_f32_bf16(const float* x, void* y, long long n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RR_H_ */

@@ -1,0 +1,127 @@
+"""Op-level parity of the HIP kernels (through the C ABI) against the CPU oracle
+and the reference golden vectors.  GPU only."""
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import cosines, golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _ops():
+    from cirtorch import _ops
+    return _ops
+
+
+def _bf16_round(t):
+    return t.to(torch.bfloat16).to(torch.float32)
+
+
+CONV_CASES = [
+    # n, cin, h, w, cout, k, stride, pad, residual, leaky
+    (2, 64, 17, 19, 64, 1, 1, 0, True, True),
+    (2, 64, 16, 20, 256, 1, 1, 0, False, False),
+    (1, 128, 15, 13, 96, 1, 2, 0, False, False),
+    (2, 64, 14, 18, 64, 3, 1, 1, False, True),
+    (1, 128, 16, 16, 128, 3, 2, 1, False, True),
+    (1, 256, 7, 9, 512, 3, 1, 1, True, True),
+    (2, 3, 40, 36, 64, 7, 2, 3, False, True),   # stem, input channels padded
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_conv_fused(cuda, case, prec):
+    n, cin, h, w, cout, k, s, p, use_res, leaky = case
+    g = torch.Generator().manual_seed(hash(case) & 0xFFFF)
+    x = torch.randn(n, cin, h, w, generator=g)
+    wt = torch.randn(cout, cin, k, k, generator=g) * (2.0 / (cin * k * k)) ** 0.5
+    scale = torch.rand(cout, generator=g) + 0.5
+    shift = torch.randn(cout, generator=g) * 0.1
+    dtype = torch.float32 if prec == "fp32" else torch.bfloat16
+    if prec == "bf16":
+        x, wt = _bf16_round(x), _bf16_round(wt)
+    ref = F.conv2d(x.double(), wt.double(), stride=s, padding=p) * scale.double()[None, :, None, None] \
+        + shift.double()[None, :, None, None]
+    res = None
+    if use_res:
+        res = torch.randn(ref.shape, generator=g)
+        if prec == "bf16":
+            res = _bf16_round(res)
+        ref = ref + res.double()
+    if leaky:
+        ref = F.leaky_relu(ref, 0.01)
+    # engine layout
+    cpad = cin if cin >= 8 else (8 if prec == "bf16" else 4)
+    xe = F.pad(x.permute(0, 2, 3, 1), (0, cpad - cin)).contiguous().to(dtype).to(cuda)
+    wp = F.pad(wt.permute(0, 2, 3, 1), (0, cpad - cin)).reshape(cout, -1)
+    kp = (wp.shape[1] + 31) // 32 * 32
+    wp = F.pad(wp, (0, kp - wp.shape[1])).to(dtype).contiguous().to(cuda)
+    re = res.permute(0, 2, 3, 1).contiguous().to(dtype).to(cuda) if use_res else None
+    y = _ops().conv2d_fused(xe, wp, k, k, s, p, cout, scale.to(cuda), shift.to(cuda), residual=re, leaky=leaky)
+    got = y.float().permute(0, 3, 1, 2).cpu().double()
+    assert got.shape == ref.shape
+    err = (got - ref).abs().max().item()
+    scale_ref = ref.abs().max().item()
+    # fp32: exact-f32 MFMA chain (K <= 2304): ~1e-6 relative; bf16 output rounding: 2^-8 relative
+    tol = 2e-5 * scale_ref if prec == "fp32" else 8e-3 * scale_ref
+    assert err <= tol, (err, scale_ref)
+
+
+def test_maxpool(cuda):
+    x = torch.randn(2, 21, 19, 64)
+    y = _ops().maxpool2d(x.to(cuda), 3, 2, 1).cpu()
+    ref = F.max_pool2d(x.permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
+    assert torch.equal(y, ref)
+
+
+def test_resize_bilinear(cuda):
+    x = torch.rand(3, 37, 50)
+    for s in (0.5, 2.0, 1 / 2 ** 0.5):
+        got = _ops().resize_bilinear(x.to(cuda), s).cpu()
+        ref = F.interpolate(x[None], scale_factor=s, mode="bilinear", align_corners=False)[0]
+        assert got.shape == ref.shape
+        assert (got - ref).abs().max() < 1e-5
+
+
+def test_pool_ops_vs_reference_golden(cuda):
+    from cirtorch.layers import functional as LF
+    g = golden("ops.npz")
+    x = torch.from_numpy(g["x"]).to(cuda)
+    for p in (3.0, 2.5):
+        got = LF.gem(x, p=p).cpu().numpy()
+        np.testing.assert_allclose(got, g["gem_p%g" % p], rtol=2e-6, atol=1e-7)
+    np.testing.assert_allclose(LF.mac(x).cpu().numpy(), g["mac"], rtol=0, atol=0)
+    np.testing.assert_allclose(LF.spoc(x).cpu().numpy(), g["spoc"], rtol=2e-6, atol=1e-7)
+    # NHWC (channels_last) input gives the same result
+    xc = x.contiguous(memory_format=torch.channels_last)
+    np.testing.assert_allclose(LF.gem(xc, p=3.0).cpu().numpy(), g["gem_p3"], rtol=2e-6, atol=1e-7)
+    np.testing.assert_allclose(LF.l2n(torch.from_numpy(g["l2n_x"]).to(cuda)).cpu().numpy(), g["l2n"],
+                               rtol=2e-6, atol=1e-7)
+
+
+def test_global_head_vs_reference_golden(cuda):
+    from cirtorch.modules.heads.global_head import globalHead
+    from oracle import weights
+    g = golden("ops.npz")
+    head = globalHead(pooling={"name": "GeM", "params": {"p": 3, "eps": 1e-6}},
+                      normal={"name": "L2N", "params": {}}, dim=512)
+    head.load_state_dict({k: torch.from_numpy(v) for k, v in weights.head_state(512).items()})
+    head = head.to(cuda)
+    x = torch.from_numpy(g["head_x"]).to(cuda)
+    np.testing.assert_allclose(head(x).cpu().numpy(), g["head"], rtol=1e-5, atol=2e-7)
+    np.testing.assert_allclose(head(x, do_whitening=False).cpu().numpy(), g["head_nowhiten"], rtol=1e-5, atol=2e-7)
+
+
+def test_whitenapply_vs_reference_golden(cuda):
+    from cirtorch.utils.whiten import whitenapply
+    from oracle import data
+    g = golden("whiten.npz")
+    X = data.unit_rows(600, 64, seed=601).T.astype(np.float32)
+    Y = whitenapply(X, g["m32"], g["P32"], dimensions=32)
+    np.testing.assert_allclose(Y, g["Y32"], rtol=1e-4, atol=2e-6)
+    Yf = whitenapply(X, g["m"].astype(np.float32), g["P"].astype(np.float32))
+    assert cosines(Yf, g["Y"]).min() > 1 - 1e-5

@@ -1,0 +1,92 @@
+"""kNN parity on the GPU: top-k indices identical to the reference
+(np.dot + np.argsort, tests/golden/knn.npz), scores within fp32 rounding of
+the reference's, full ranks identical to np.argsort for mAP, shard merge
+bit-identical to the single-GPU result."""
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("tag", ["4k", "100k"])
+def test_knn_vs_reference_golden(cuda, precision, tag):
+    from cirtorch.search import KnnIndex
+    from oracle import data
+    g = golden("knn.npz")
+    n, q, k = (int(v) for v in g["shape_" + tag])
+    db = torch.from_numpy(data.database(n)).to(cuda)
+    qq = torch.from_numpy(data.queries(q, seed=int(g["qseed_" + tag]))).to(cuda)
+    s, i = KnnIndex(db, precision).search(qq, k)
+    np.testing.assert_array_equal(i.cpu().numpy(), g["idx_" + tag])
+    np.testing.assert_allclose(s.cpu().numpy(), g["score_" + tag], rtol=0, atol=2e-7)
+
+
+def test_knn_matches_exact_oracle_random_shapes(cuda):
+    from cirtorch.search import KnnIndex
+    from oracle import data, ops
+    for n, q, d, k in ((1, 3, 64, 1), (37, 5, 128, 10), (16384, 3, 256, 64), (40000, 9, 512, 100), (70001, 2, 64, 7)):
+        db = data.unit_rows(n, d, seed=n)
+        qq = data.unit_rows(q, d, seed=n + 1)
+        kk = min(k, n)
+        ref_s, ref_i = ops.topk_exact(db, qq, kk)
+        for prec in ("fp32", "bf16"):
+            s, i = KnnIndex(torch.from_numpy(db).to(cuda), prec).search(torch.from_numpy(qq).to(cuda), kk)
+            np.testing.assert_array_equal(i.cpu().numpy(), ref_i, err_msg="%s %s" % (prec, (n, q, d, k)))
+            np.testing.assert_allclose(s.cpu().numpy(), ref_s, rtol=0, atol=1e-12)
+
+
+def test_knn_ties_lower_index_first(cuda):
+    """Duplicated rows give exactly equal scores: ties resolve to the lower index."""
+    from cirtorch.search import KnnIndex
+    from oracle import data, ops
+    base = data.unit_rows(50, 128, seed=3)
+    db = np.concatenate([base, base, base[:10]], 0)  # rows i, i+50 identical
+    qq = data.unit_rows(4, 128, seed=4)
+    ref_s, ref_i = ops.topk_exact(db, qq, 20)
+    s, i = KnnIndex(torch.from_numpy(db).to(cuda), "fp32").search(torch.from_numpy(qq).to(cuda), 20)
+    np.testing.assert_array_equal(i.cpu().numpy(), ref_i)
+
+
+def test_knn_k_larger_than_db(cuda):
+    from cirtorch.search import KnnIndex
+    from oracle import data
+    db = data.unit_rows(5, 64, seed=9)
+    qq = data.unit_rows(2, 64, seed=10)
+    s, i = KnnIndex(torch.from_numpy(db).to(cuda), "fp32").search(torch.from_numpy(qq).to(cuda), 8)
+    i = i.cpu().numpy()
+    assert (i[:, 5:] == -1).all() and sorted(i[0, :5].tolist()) == list(range(5))
+
+
+def test_rank_full_equals_argsort(cuda):
+    from cirtorch.search import rank
+    g = golden("map.npz")
+    from oracle import data
+    db = data.unit_rows(700, 256, seed=21)
+    qq = data.unit_rows(6, 256, seed=22)
+    ranks = rank(torch.from_numpy(db.T.copy()), torch.from_numpy(qq.T.copy())).cpu().numpy()
+    ref = np.argsort(-np.dot(db.astype(np.float64), qq.astype(np.float64).T), axis=0, kind="stable")
+    np.testing.assert_array_equal(ranks, ref)
+    assert g["ranks"].shape == (4993, 70)
+
+
+def test_topk_merge_equals_single_shard(cuda):
+    from cirtorch.search import KnnIndex, merge_topk
+    from oracle import data
+    n, q, d, k, R = 30000, 6, 256, 50, 4
+    db = torch.from_numpy(data.unit_rows(n, d, seed=31)).to(cuda)
+    qq = torch.from_numpy(data.unit_rows(q, d, seed=32)).to(cuda)
+    s1, i1 = KnnIndex(db, "bf16").search(qq, k)
+    per = (n + R - 1) // R
+    ss, ii = [], []
+    for r in range(R):
+        sl = db[r * per:(r + 1) * per]
+        s, i = KnnIndex(sl, "bf16", idx_offset=r * per).search(qq, k)
+        ss.append(s)
+        ii.append(i)
+    sm, im = merge_topk(torch.stack(ss), torch.stack(ii), k)
+    assert torch.equal(im, i1) and torch.equal(sm, s1)
