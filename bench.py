@@ -1,0 +1,259 @@
+#!/usr/bin/env python
+"""Extract-and-match benchmark (BASELINE.json metric).
+
+One step (per rank): extract B synthetic 3x768x1024 images with ResNet50-GeM
+(+ whitening head) in bf16 on the MFMA engine, all-gather the B x world query
+descriptors, search them (top-100 cosine kNN, exact ordering) against a
+1M x 2048 database sharded over the ranks (per-shard top-k -> RCCL all-gather
+-> on-GPU merge).  Per-rank work is fixed as ranks grow (images per rank,
+and queries x local rows per rank), so scaling is weak.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Rank 0 prints ONE JSON line.  Also measured (separate loops, same process):
+extract-only images/s and kNN-only queries/s at Q=1024 against the 1M DB.
+The CPU baseline (rank 0, N=1 only) times the oracle restatement of the
+reference path on a bounded sample (oracle/ is the checker, not the product).
+"""
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "image-retrieval-for-image-based-localization_amd")
+for _p in (PKG, REPO):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_F32_TFLOPS = 157.3     # exact-f32 MFMA
+PEAK_HBM_GBS = 8000.0
+METRIC = "images/sec extract + queries/sec 1M-desc kNN, ResNet50-GeM 1024×768"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=8, help="images per rank per step")
+    ap.add_argument("--height", type=int, default=768)
+    ap.add_argument("--width", type=int, default=1024)
+    ap.add_argument("--arch", default="resnet50")
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--db-rows", type=int, default=1_000_000)
+    ap.add_argument("--dim", type=int, default=2048)
+    ap.add_argument("--k", type=int, default=100)
+    ap.add_argument("--knn-q", type=int, default=1024, help="queries for the kNN-only sub-benchmark (0 = skip)")
+    ap.add_argument("--knn-steps", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-images", type=int, default=2)
+    ap.add_argument("--cpu-db-rows", type=int, default=100_000)
+    return ap.parse_args()
+
+
+def conv_flops_per_image(body, h, w):
+    """2 x MACs of every conv of the body at input h x w (algorithmic FLOPs)."""
+    tot = 0
+    hh, ww = h, w
+
+    def out(s, k, st, p):
+        return (s + 2 * p - k) // st + 1
+
+    c = body.mod1.conv1
+    hh, ww = out(hh, 7, 2, 3), out(ww, 7, 2, 3)
+    tot += 2 * hh * ww * c.out_channels * c.in_channels * 49
+    hh, ww = out(hh, 3, 2, 1), out(ww, 3, 2, 1)
+    for m in range(2, 6):
+        for blk in getattr(body, "mod%d" % m).children():
+            convs = [blk.convs.conv1, blk.convs.conv2] + ([blk.convs.conv3] if blk.is_bottleneck else [])
+            h0, w0 = hh, ww
+            for cv in convs:
+                k, st, p = cv.kernel_size[0], cv.stride[0], cv.padding[0]
+                hh, ww = out(hh, k, st, p), out(ww, k, st, p)
+                tot += 2 * hh * ww * cv.out_channels * cv.in_channels * k * k
+            if hasattr(blk, "proj_conv"):
+                cv = blk.proj_conv
+                tot += 2 * out(h0, 1, cv.stride[0], 0) * out(w0, 1, cv.stride[0], 0) * cv.out_channels * cv.in_channels
+    return tot
+
+
+def cpu_baseline(args):
+    """Oracle restatement of the reference CPU path, timed on this host."""
+    import numpy as np
+    from oracle import backbone as obb, data, weights
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    net = obb.OracleNet(args.arch, weights.backbone_state(args.arch), weights.head_state(weights.OUTPUT_DIM[args.arch]))
+    imgs = torch.from_numpy(data.images(args.cpu_images, args.height, args.width))
+    with torch.no_grad():
+        net.forward_padded(imgs[:1])  # warm
+        t0 = time.perf_counter()
+        for i in range(args.cpu_images):
+            net.forward_padded(imgs[i:i + 1])     # reference test batch size is 1 (base.ini:143)
+        t_ext = (time.perf_counter() - t0) / args.cpu_images
+    db = data.database(args.cpu_db_rows, args.dim)
+    q = data.queries(8, args.dim)
+    t0 = time.perf_counter()
+    scores = np.dot(db, q.T)                      # scripts/test.py:247
+    ranks = np.argsort(-scores, axis=0)           # scripts/test.py:248
+    t_match = (time.perf_counter() - t0) / q.shape[0] * (args.db_rows / args.cpu_db_rows)
+    del ranks
+    per_img = t_ext + t_match
+    return {"value": 1.0 / per_img, "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": ("oracle restatement (torch-CPU conv/BN/leaky + GeM/L2N/whiten) of %d x 3x%dx%d images "
+                       "at batch 1 (%.3f s/img) + np.dot/np.argsort over a %d-row sample DB, 8 queries, scaled "
+                       "x%.0f to %d rows (%.3f s/query); host %s"
+                       % (args.cpu_images, args.height, args.width, t_ext, args.cpu_db_rows,
+                          args.db_rows / args.cpu_db_rows, args.db_rows, t_match, platform.processor() or "cpu"))}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from cirtorch import _ops
+    from cirtorch.models.GF_net import make_net
+    from cirtorch.models.init import random_init_
+    from cirtorch.search import ShardedIndex
+
+    net = make_net(args.arch, precision=args.precision, mean=[0.485, 0.456, 0.406], std=[0.229, 0.224, 0.225])
+    random_init_(net, seed=0)
+    net = net.to(dev).eval()
+    B, H, W = args.batch, args.height, args.width
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    images = torch.rand((B, 3, H, W), generator=g, device=dev)
+
+    per = (args.db_rows + world - 1) // world
+    r0 = rank * per
+    n_local = max(0, min(per, args.db_rows - r0))
+    db32 = _ops.fill_unit_rows(n_local, args.dim, seed=0xDB5EED, row0=r0, device=dev)
+    index = ShardedIndex(db32, r0, precision=args.precision)
+
+    ev_pairs = []
+
+    def step(record):
+        e0 = e1 = None
+        if record:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        desc = net.extract(images)                  # D x B (on-device, fp32)
+        if record:
+            e1.record()
+            ev_pairs.append((e0, e1))
+        q = desc.t().contiguous()
+        if world > 1:
+            qa = torch.empty((world * B, q.shape[1]), dtype=q.dtype, device=dev)
+            dist.all_gather_into_tensor(qa, q)
+            q = qa
+        return index.search(q, args.k)
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            step(False)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step(True)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([elapsed], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        body_ms = sum(a.elapsed_time(b) for a, b in ev_pairs) / len(ev_pairs)
+
+        # extract-only loop (same net, no matching)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(max(3, args.steps // 2)):
+            net.extract(images)
+        torch.cuda.synchronize()
+        ext_only = max(3, args.steps // 2) * B / (time.perf_counter() - t1)
+
+        # kNN-only loop: Q queries (same on every rank) vs the sharded 1M DB
+        knn = None
+        if args.knn_q > 0:
+            qk = _ops.fill_unit_rows(args.knn_q, args.dim, seed=0x0E5EED, row0=0, device=dev)
+            index.search(qk, args.k)
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            t2 = time.perf_counter()
+            for _ in range(args.knn_steps):
+                index.search(qk, args.k)
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            tk = (time.perf_counter() - t2) / args.knn_steps
+            if world > 1:
+                t = torch.tensor([tk], device=dev)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                tk = float(t.item())
+            flops = 2.0 * args.knn_q * n_local * args.dim
+            peak = PEAK_BF16_TFLOPS if args.precision == "bf16" else PEAK_F32_TFLOPS
+            knn = {"queries_per_sec": args.knn_q / tk, "q": args.knn_q, "db_rows": args.db_rows, "k": args.k,
+                   "ms_per_batch": tk * 1e3,
+                   "roofline": {"bound": "mfma", "achieved": flops / tk / 1e12, "peak": peak, "unit": "TFLOP/s",
+                                "frac": flops / tk / 1e12 / peak, "traffic": None,
+                                "note": "per-rank screening GEMM FLOPs 2*Q*n_local*D / whole search time"}}
+
+    fl_img = conv_flops_per_image(net.body, H, W)
+    achieved = fl_img * B / (body_ms * 1e-3) / 1e12
+    peak = PEAK_BF16_TFLOPS if args.precision == "bf16" else PEAK_F32_TFLOPS
+    value = world * B * args.steps / elapsed
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "images/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.precision,
+        "data": "synthetic (U[0,1) images, random-init weights, counter-hash N(0,1) unit DB rows)",
+        "config": {"workload": "%s-GeM+whiten %s extract %dx%d, B=%d/GPU, then top-%d cosine kNN of all %d queries "
+                               "vs %d x %d DB sharded over %d GPU(s)" % (args.arch, args.precision, W, H, B, args.k,
+                                                                        B * world, args.db_rows, args.dim, world),
+                   "global_batch": B * world, "image": [3, H, W], "db_rows": args.db_rows, "dim": args.dim,
+                   "k": args.k, "parallelism": "dp%d (images) x db-shard%d" % (world, world)},
+        "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                     "frac": achieved / peak, "traffic": None,
+                     "note": "dominant kernel = k_conv (implicit-GEMM MFMA conv family, 53 launches/forward); "
+                             "%.2f GFLOP/img x %d img / extract-body event time %.3f ms" % (fl_img / 1e9, B, body_ms)},
+        "extract_images_per_sec": ext_only * world,
+        "knn": knn,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args)
+    if rank == 0:
+        print(json.dumps(out))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -84,6 +84,12 @@ class ImageRetrievalNet(nn.Module):
                 do_loss=False, do_prediction=True, **varargs):
         if do_loss:
             raise NotImplementedError("training (tuple loss) is out of scope for the MI355X engine")
+        if isinstance(img, torch.Tensor) and img.dim() == 4 and len(scales) == 1:
+            # already a same-size batch: no packing / padding copy
+            x = self.body(img, normalize=self._normalizer())
+            ret_pred = self.ret_algo.inference(self.ret_head, x, [img.shape[-2:]] * img.shape[0]) \
+                if do_prediction else None
+            return OrderedDict([("ret_loss", None)]), OrderedDict([("ret_pred", ret_pred)])
         if isinstance(img, torch.Tensor):
             img = PackedSequence(list(img)) if img.dim() == 4 else PackedSequence([img])
         if len(scales) > 1:
@@ -105,8 +111,11 @@ class ImageRetrievalNet(nn.Module):
 
     # upstream-style single call: list of [3, H, W] tensors -> D x N
     def extract(self, images, scales=(1,)):
+        """images: list of [3, H, W] tensors or one [N, 3, H, W] batch -> D x N."""
+        if not isinstance(images, torch.Tensor):
+            images = PackedSequence(list(images))
         with torch.no_grad():
-            _, pred = self.forward(img=PackedSequence(list(images)), scales=list(scales))
+            _, pred = self.forward(img=images, scales=list(scales))
         return pred["ret_pred"]
 
 

@@ -13,7 +13,7 @@ from conftest import cosines, golden
 pytestmark = pytest.mark.gpu
 
 FP32_COS = 1 - 1e-4      # north_star parity bar (fp32)
-BF16_COS = 1 - 2e-2      # bf16 operands through 50-150 layers (measured)
+BF16_COS = 1 - 2e-3      # bf16 operands/activations through 20-100 layers (measured 0.9993-0.9995)
 
 
 def product_net(arch, head_bias, precision, cuda):
@@ -98,8 +98,8 @@ def test_stage_checksums_r18(cuda):
     from oracle import data
     g = golden("r18.npz")
     net = product_net("resnet18", g["head_bias"], "fp32", cuda)
-    imgs = data.structured_images(1, *[int(v) for v in g["res"]], seed=int(g["seed"]))
-    x = normalized(imgs, cuda)[0][None]
+    imgs = data.structured_images(int(g["n"]), *[int(v) for v in g["res"]], seed=int(g["seed"]))
+    x = normalized(imgs[:1], cuda)[0][None]
     with torch.no_grad():
         outs = net.body(x)
     for k in ("mod1", "mod2", "mod3", "mod4", "mod5"):
