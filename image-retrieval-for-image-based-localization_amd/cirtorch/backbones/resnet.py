@@ -160,7 +160,7 @@ class ResNet(nn.Module):
         if cin_pad > ci:
             wp = F.pad(wp, (0, cin_pad - ci))
         wp = wp.reshape(co, kh * kw * cin_pad)
-        kp = (wp.shape[1] + 31) // 32 * 32
+        kp = (wp.shape[1] + 63) // 64 * 64  # 128-B K-steps for the LDS-DMA engine
         if kp > wp.shape[1]:
             wp = F.pad(wp, (0, kp - wp.shape[1]))
         st.w = wp.to(self.engine_dtype).contiguous()

@@ -24,6 +24,8 @@
 // of the kNN (scripts/test.py:247).
 #include "rr_internal.h"
 
+#include <cstdlib>
+
 namespace rr {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
@@ -273,9 +275,30 @@ static void launch(const ConvArgs& a, bool k1, hipStream_t s) {
         launch_cfg<T, TO, 128, 128, 2, 2>(a, k1, s);
 }
 
+template <typename T, typename TO> void launch_gemm2(const ConvArgs& a, bool k1, hipStream_t s);
+
+// v2 (LDS-DMA) engine eligibility: 128-byte K-steps and 31-bit buffer offsets.
+static bool use_v2(const ConvArgs& a, int dtype) {
+    static int forced = -1;
+    if (forced < 0) {
+        const char* e = getenv("RR_GEMM_V1");
+        forced = (e && e[0] == '1') ? 1 : 0;
+    }
+    if (forced == 1) return false;
+    const int esz = dtype == RR_BF16 ? 2 : 4;
+    const long long xbytes = (long long)a.n * a.h * a.w_ * a.cin * esz;
+    return (a.kp * esz) % 128 == 0 && xbytes < (1ll << 31) && (long long)256 * a.kp * esz < (1ll << 31);
+}
+
+template <typename T, typename TO>
+static void dispatch(const ConvArgs& a, bool k1, int dtype, hipStream_t s) {
+    if (use_v2(a, dtype)) launch_gemm2<T, TO>(a, k1, s);
+    else launch<T, TO>(a, k1, s);
+}
+
 void gemm_scores(const ConvArgs& a, int dtype, hipStream_t s) {
-    if (dtype == RR_BF16) launch<bf16_t, float>(a, true, s);
-    else launch<float, float>(a, true, s);
+    if (dtype == RR_BF16) dispatch<bf16_t, float>(a, true, dtype, s);
+    else dispatch<float, float>(a, true, dtype, s);
 }
 
 }  // namespace rr
@@ -311,9 +334,9 @@ extern "C" int rr_conv2d_fused(const void* x, const void* w, const float* scale,
     // 1x1 / pad 0: every K-run of a pixel is contiguous -> no im2col index math.
     const bool k1 = d->kh == 1 && d->kw == 1 && d->pad == 0 && d->k_packed == d->c_in;
     hipStream_t s = as_stream(stream);
-    if (dtype == RR_BF16 && out_dtype == RR_BF16) launch<bf16_t, bf16_t>(a, k1, s);
-    else if (dtype == RR_BF16 && out_dtype == RR_F32) launch<bf16_t, float>(a, k1, s);
-    else if (dtype == RR_F32 && out_dtype == RR_F32) launch<float, float>(a, k1, s);
+    if (dtype == RR_BF16 && out_dtype == RR_BF16) dispatch<bf16_t, bf16_t>(a, k1, dtype, s);
+    else if (dtype == RR_BF16 && out_dtype == RR_F32) dispatch<bf16_t, float>(a, k1, dtype, s);
+    else if (dtype == RR_F32 && out_dtype == RR_F32) dispatch<float, float>(a, k1, dtype, s);
     else return fail(RR_EINVAL, "rr_conv2d_fused: unsupported dtype pair");
     return check_launch("rr_conv2d_fused");
 }

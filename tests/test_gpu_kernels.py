@@ -58,7 +58,7 @@ def test_conv_fused(cuda, case, prec):
     cpad = cin if cin >= 8 else (8 if prec == "bf16" else 4)
     xe = F.pad(x.permute(0, 2, 3, 1), (0, cpad - cin)).contiguous().to(dtype).to(cuda)
     wp = F.pad(wt.permute(0, 2, 3, 1), (0, cpad - cin)).reshape(cout, -1)
-    kp = (wp.shape[1] + 31) // 32 * 32
+    kp = (wp.shape[1] + 63) // 64 * 64
     wp = F.pad(wp, (0, kp - wp.shape[1])).to(dtype).contiguous().to(cuda)
     re = res.permute(0, 2, 3, 1).contiguous().to(dtype).to(cuda) if use_res else None
     y = _ops().conv2d_fused(xe, wp, k, k, s, p, cout, scale.to(cuda), shift.to(cuda), residual=re, leaky=leaky)
