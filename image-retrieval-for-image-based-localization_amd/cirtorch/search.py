@@ -73,25 +73,45 @@ def rank(vecs, qvecs, precision="fp32"):
     return ranks
 
 
+def shard_range(n, rank, world):
+    """Contiguous row shard of rank r: [r*ceil(n/R), min(n, (r+1)*ceil(n/R)))."""
+    per = (n + world - 1) // world
+    r0 = min(n, rank * per)
+    return r0, max(0, min(per, n - r0))
+
+
+def all_gather_stacked(t, group=None):
+    """[...] per rank -> [R, ...] on every rank (RCCL all-gather on GPU tensors)."""
+    world = dist.get_world_size(group)
+    out = torch.empty((world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+    if t.is_cuda:
+        dist.all_gather_into_tensor(out, t.contiguous(), group=group)
+    else:
+        dist.all_gather(list(out.unbind(0)), t.contiguous(), group=group)
+    return out
+
+
 class ShardedIndex:
     """Database rows [row0, row0 + n_local) of a global matrix live on this
     rank; ``search`` expects the same queries on every rank (all-gather them
-    first if each rank extracted its own)."""
+    first if each rank extracted its own).
 
-    def __init__(self, local_rows, row0, precision="bf16", cand=0, group=None):
-        self.local = KnnIndex(local_rows, precision, cand, idx_offset=row0)
+    The only exchange is one all-gather of the per-shard (score f64, index i64)
+    lists — Q x k x 16 bytes per rank — followed by the on-GPU merge with the
+    (score desc, index asc) rule, so the merged result is bit-identical to a
+    single-GPU search of the whole database."""
+
+    def __init__(self, local_rows, row0, precision="bf16", cand=0, group=None, local_index=None, merge=None):
+        self.local = local_index if local_index is not None else KnnIndex(local_rows, precision, cand, idx_offset=row0)
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.merge = merge or _ops.topk_merge
 
     def search(self, q_rows, k):
         s, i = self.local.search(q_rows, k)
         if self.world == 1:
             return s, i
-        gs = torch.empty((self.world,) + tuple(s.shape), dtype=s.dtype, device=s.device)
-        gi = torch.empty((self.world,) + tuple(i.shape), dtype=i.dtype, device=i.device)
-        dist.all_gather_into_tensor(gs, s.contiguous(), group=self.group)
-        dist.all_gather_into_tensor(gi, i.contiguous(), group=self.group)
-        return _ops.topk_merge(gs, gi, k)
+        return self.merge(all_gather_stacked(s, self.group), all_gather_stacked(i, self.group), k)
 
 
 def merge_topk(scores, idx, k):

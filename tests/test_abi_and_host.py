@@ -1,0 +1,162 @@
+"""CPU checks of the C ABI (library loads, every header symbol exported and
+bound) and of the host-side mirror of the reference interface (no GPU
+compute calls here)."""
+
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import PKG, REPO, golden
+
+HEADER = os.path.join(REPO, "include", "rr.h")
+LIB = os.path.join(PKG, "librr.so")
+
+
+def header_symbols():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:[\w\*\s]+?)\b(rr_\w+)\s*\(", text, flags=re.M)))
+
+
+def test_library_exports_every_header_symbol():
+    if not os.path.exists(LIB):
+        pytest.skip("librr.so not built (run __graft_entry__.build())")
+    syms = header_symbols()
+    assert len(syms) >= 15
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\b(rr_\w+)\b", out))
+    missing = [s for s in syms if s not in exported]
+    assert not missing, missing
+
+
+def test_ctypes_binding_covers_header():
+    if not os.path.exists(LIB):
+        pytest.skip("librr.so not built")
+    from cirtorch import _engine
+    lib = _engine.lib()
+    assert set(header_symbols()) == set(_engine._SIGS), set(header_symbols()) ^ set(_engine._SIGS)
+    assert lib.rr_version() >= 1
+    assert lib.rr_knn_workspace_bytes(1000, 4, 512, 10, 0, _engine.RR_F32) > 0
+
+
+def test_conv_desc_layout_matches_header():
+    from cirtorch import _engine
+    text = open(HEADER).read()
+    body = re.search(r"typedef struct rr_conv_desc \{(.*?)\} rr_conv_desc;", text, re.S).group(1)
+    fields = []
+    for line in body.splitlines():
+        line = line.split("/*")[0].strip().rstrip(";")
+        if not line:
+            continue
+        typ, names = line.split(None, 1)
+        fields += [(n.strip(), typ) for n in names.split(",")]
+    assert [f[0] for f in fields] == [f[0] for f in _engine.ConvDesc._fields_]
+
+
+def test_error_path_reports_message():
+    if not os.path.exists(LIB):
+        pytest.skip("librr.so not built")
+    from cirtorch import _engine
+    lib = _engine.lib()
+    rc = lib.rr_l2n_rows(None, 0, 0, 1e-6, None, None)
+    assert rc != 0 and b"rr_l2n_rows" in lib.rr_last_error()
+
+
+def test_product_refuses_cpu_tensors():
+    from cirtorch.layers import functional as LF
+    with pytest.raises(RuntimeError, match="GPU"):
+        LF.gem(torch.rand(1, 8, 3, 3))
+    from cirtorch.models.GF_net import make_net
+    net = make_net("resnet18", precision="fp32")
+    with pytest.raises(RuntimeError, match="GPU"):
+        net.extract([torch.rand(3, 32, 32)])
+
+
+def test_backbone_state_dict_matches_reference_layout():
+    """Our module tree accepts the reference key layout exactly (oracle weights use it)."""
+    from cirtorch.backbones import resnet
+    from oracle import weights
+    for arch in ("resnet18", "resnet50", "resnet101"):
+        body = resnet.__dict__[arch]()
+        sd = {k: torch.from_numpy(v) for k, v in weights.backbone_state(arch).items()}
+        missing, unexpected = body.load_state_dict(sd, strict=False)
+        assert not missing and not unexpected, (arch, missing[:3], unexpected[:3])
+
+
+def test_convert_torchvision_keys():
+    from cirtorch.backbones import resnet
+    body = resnet.resnet50()
+    tv = {}
+    for k, v in body.state_dict().items():
+        k2 = k.replace("mod1.conv1", "conv1").replace("mod1.bn1", "bn1")
+        m = re.match(r"mod(\d)\.block(\d+)\.(.*)", k2)
+        if m:
+            mod, blk, rest = int(m.group(1)), int(m.group(2)), m.group(3)
+            rest = rest.replace("convs.", "").replace("proj_conv", "downsample.0").replace("proj_bn", "downsample.1")
+            k2 = "layer%d.%d.%s" % (mod - 1, blk - 1, rest)
+        tv[k2] = v
+    out = body.convert(tv)
+    assert set(out) == {k for k in body.state_dict() if not k.endswith("num_batches_tracked")}
+
+
+def test_packed_sequence_and_padding():
+    from cirtorch.utils.parallel import PackedSequence
+    from cirtorch.utils.sequence import pad_packed_images, pack_padded_images
+    a, b = torch.rand(3, 5, 7), torch.rand(3, 6, 4)
+    ps = PackedSequence([a, b])
+    padded, sizes = pad_packed_images(ps)
+    assert padded.shape == (2, 3, 6, 7)
+    assert torch.equal(padded[0, :, :5, :7], a) and torch.equal(padded[1, :, :6, :4], b)
+    assert padded[0, :, 5:].abs().sum() == 0 and padded[1, :, :, 4:].abs().sum() == 0
+    back = pack_padded_images(padded, sizes)
+    assert torch.equal(back[0], a) and torch.equal(back[1], b)
+    with pytest.raises(ValueError):
+        pad_packed_images(PackedSequence([torch.rand(3, 4, 4), torch.rand(1, 4, 4)]))
+    with pytest.raises(TypeError):
+        PackedSequence([a, b.double()])
+
+
+def test_map_evaluation_host_code_matches_reference_golden():
+    from cirtorch.utils.evaluation.ParisOxfordEval import compute_map_and_print
+    g = golden("map.npz")
+    from test_oracle_golden import _gnd
+    gnd = _gnd(g)
+    logs = []
+    score = compute_map_and_print("roxford5k", g["ranks"].astype(np.int64), gnd, lambda *a: logs.append(a))
+    assert score["mAP"] == pytest.approx(float(g["score_mAP"]), abs=1e-10)
+    assert score["mapE"] == pytest.approx(float(g["mapE"]), abs=1e-12)
+
+
+def test_upstream_surface_imports():
+    """Every name scripts/test.py imports (scripts/test.py:12-18) resolves."""
+    from cirtorch.models.GF_net import init_network, extract_vectors  # noqa: F401
+    from cirtorch.datasets.datahelpers import cid2filename
+    from cirtorch.datasets.testdataset import configdataset  # noqa: F401
+    from cirtorch.utils.download import download_train, download_test  # noqa: F401
+    from cirtorch.utils.whiten import whitenlearn, whitenapply  # noqa: F401
+    from cirtorch.utils.evaluate import compute_map_and_print  # noqa: F401
+    from cirtorch.utils.general import get_data_root, htime
+    from cirtorch.layers.pooling import GeM, MAC, SPoC  # noqa: F401
+    from cirtorch.layers.normalization import L2N  # noqa: F401
+    from cirtorch.modules.pools import POOLING_LAYERS
+    from cirtorch.modules.normalizations import NORMALIZATION_LAYERS
+    assert cid2filename("abcdef123", "/r") == "/r/23/f1/de/abcdef123"
+    assert htime(3725) == "1h 2m 5s"
+    assert get_data_root().endswith("data")
+    assert {"GeM", "MAC", "SPoC"} <= set(POOLING_LAYERS) and "L2N" in NORMALIZATION_LAYERS
+    net = init_network({"architecture": "resnet50", "pooling": "gem", "whitening": True,
+                        "mean": [0.485, 0.456, 0.406], "std": [0.229, 0.224, 0.225]})
+    assert abs(float(net.pool.p.item()) - 3.0) < 1e-7 and "architecture" in net.meta_repr()
+
+
+def test_whitenlearn_host_matches_reference_golden():
+    from cirtorch.utils.whiten import whitenlearn
+    from oracle import data
+    g = golden("whiten.npz")
+    X = data.unit_rows(600, 64, seed=601).T.astype(np.float64)
+    m, P = whitenlearn(X, g["qidxs"], g["pidxs"])
+    np.testing.assert_allclose(m, g["m"], rtol=1e-12)
+    np.testing.assert_allclose(np.abs(P), np.abs(g["P"]), rtol=1e-6, atol=1e-8)
