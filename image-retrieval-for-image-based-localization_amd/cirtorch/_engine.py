@@ -20,7 +20,7 @@ LIB_PATH = os.environ.get("RR_LIB", os.path.join(PKG_DIR, "librr.so"))
 RR_F32, RR_BF16 = 0, 1
 RR_ACT_IDENTITY, RR_ACT_LEAKY = 0, 1
 RR_POOL_GEM, RR_POOL_MAC, RR_POOL_SPOC = 0, 1, 2
-RR_CONV_AFFINE, RR_CONV_RESIDUAL = 1, 2
+RR_CONV_AFFINE, RR_CONV_RESIDUAL, RR_CONV_PERM32 = 1, 2, 4
 RR_NHWC, RR_NCHW = 0, 1
 
 _DTYPE_CODE = {torch.float32: RR_F32, torch.bfloat16: RR_BF16}
@@ -39,6 +39,7 @@ _SIGS = {
     "rr_device_arch": ([ctypes.c_char_p, _i], _i),
     "rr_image_to_nhwc": ([_vp, _i, _i, _i, _i, ctypes.POINTER(_f), ctypes.POINTER(_f), _i, _vp, _i, _i, _vp], _i),
     "rr_conv2d_fused": ([_vp, _vp, _vp, _vp, _vp, _vp, ctypes.POINTER(ConvDesc), _i, _i, _vp], _i),
+    "rr_pack_conv_weights": ([_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _vp], _i),
     "rr_maxpool2d": ([_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _i, _vp], _i),
     "rr_resize_bilinear": ([_vp, _i, _i, _i, _vp, _i, _i, _d, _d, _vp], _i),
     "rr_global_pool": ([_vp, _i, _i, _i, _i, _i, _f, _f, _vp, _i, _vp], _i),

@@ -32,9 +32,22 @@ def image_to_nhwc(img, c_pad, dtype, mean=None, std=None):
     return out
 
 
+def pack_conv_weights(weight, cin_pad, dtype, perm32=False, k_mult=64):
+    """nn.Conv2d weight [c_out, c_in, kh, kw] (GPU) -> engine layout [c_out, k_packed]."""
+    E.require_gpu(weight)
+    w = weight.detach().float().contiguous()
+    co, ci, kh, kw = w.shape
+    kp = (kh * kw * cin_pad + k_mult - 1) // k_mult * k_mult
+    out = torch.empty((co, kp), dtype=dtype, device=w.device)
+    E.check(E.lib().rr_pack_conv_weights(E.ptr(w), co, ci, kh, kw, cin_pad, kp, int(bool(perm32)), E.ptr(out),
+                                         E.dtype_code(dtype), _st()), "rr_pack_conv_weights")
+    return out
+
+
 def conv2d_fused(x, w_packed, kh, kw, stride, pad, c_out, scale=None, shift=None, residual=None,
-                 leaky=True, slope=0.01, out_dtype=None, dil=1):
-    """x: [N, H, W, C] -> act(conv(x) * scale + shift (+ residual)) as [N, Ho, Wo, c_out]."""
+                 leaky=True, slope=0.01, out_dtype=None, dil=1, perm32=False):
+    """x: [N, H, W, C] -> act(conv(x) * scale + shift (+ residual)) as [N, Ho, Wo, c_out].
+    perm32: w_packed rows are in the RR_CONV_PERM32 order (pack_conv_weights(perm32=True))."""
     E.require_gpu(x, w_packed)
     n, h, w, c = x.shape
     ho = (h + 2 * pad - dil * (kh - 1) - 1) // stride + 1
@@ -47,6 +60,8 @@ def conv2d_fused(x, w_packed, kh, kw, stride, pad, c_out, scale=None, shift=None
     if residual is not None:
         flags |= E.RR_CONV_RESIDUAL
         assert residual.shape == y.shape and residual.dtype == out_dtype and residual.is_contiguous()
+    if perm32:
+        flags |= E.RR_CONV_PERM32
     d = E.ConvDesc(n=n, h=h, w=w, c_in=c, ho=ho, wo=wo, c_out=c_out, kh=kh, kw=kw, stride=stride, pad=pad,
                    dil=dil, k_packed=w_packed.shape[1], ldy=c_out,
                    act=E.RR_ACT_LEAKY if leaky else E.RR_ACT_IDENTITY, slope=slope, flags=flags)

@@ -45,7 +45,7 @@ def try_index(scalar_or_list, i):
 
 
 class _ConvStep:
-    __slots__ = ("w", "kh", "kw", "stride", "pad", "c_out", "scale", "shift", "leaky", "slope")
+    __slots__ = ("w", "kh", "kw", "stride", "pad", "c_out", "scale", "shift", "leaky", "slope", "perm")
 
 
 class ResNet(nn.Module):
@@ -153,17 +153,12 @@ class ResNet(nn.Module):
 
     def _step(self, conv, bn, cin_pad=None, leaky_override=None):
         st = _ConvStep()
-        w = conv.weight.detach().float()
-        co, ci, kh, kw = w.shape
+        co, ci, kh, kw = conv.weight.shape
         cin_pad = cin_pad or ci
-        wp = w.permute(0, 2, 3, 1)  # co, kh, kw, ci  (k = (kh*KW + kw)*c_in + ci)
-        if cin_pad > ci:
-            wp = F.pad(wp, (0, cin_pad - ci))
-        wp = wp.reshape(co, kh * kw * cin_pad)
-        kp = (wp.shape[1] + 63) // 64 * 64  # 128-B K-steps for the LDS-DMA engine
-        if kp > wp.shape[1]:
-            wp = F.pad(wp, (0, kp - wp.shape[1]))
-        st.w = wp.to(self.engine_dtype).contiguous()
+        # engine layout [c_out][(kh*KW + kw)*c_in + ci], 128-B K-steps, rows in the
+        # 32-row MFMA-interleaved order so each lane stores 8 consecutive channels
+        st.perm = co % 32 == 0
+        st.w = _ops.pack_conv_weights(conv.weight, cin_pad, self.engine_dtype, perm32=st.perm)
         st.kh, st.kw = kh, kw
         st.stride = conv.stride[0]
         st.pad = conv.padding[0]
@@ -199,7 +194,7 @@ class ResNet(nn.Module):
     @staticmethod
     def _conv(t, st, residual=None):
         return _ops.conv2d_fused(t, st.w, st.kh, st.kw, st.stride, st.pad, st.c_out, st.scale, st.shift,
-                                 residual=residual, leaky=st.leaky, slope=st.slope)
+                                 residual=residual, leaky=st.leaky, slope=st.slope, perm32=st.perm)
 
     def forward(self, x, normalize=None):
         """x: [N, 3, H, W] float32 on the GPU (already normalised unless

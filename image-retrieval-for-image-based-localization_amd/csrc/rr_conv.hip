@@ -206,6 +206,27 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs a) {
     const bool affine = a.flags & RR_CONV_AFFINE;
     const bool resid = a.flags & RR_CONV_RESIDUAL;
     const bool leaky = a.act == RR_ACT_LEAKY;
+    if (a.flags & RR_CONV_PERM32) {  // rows are permuted: scalar path through perm32_channel
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+                const int p = p0 + wp * (TP / WP) + j * 16 + r16;
+                if (p >= a.P) continue;
+                for (int r = 0; r < 4; ++r) {
+                    const int row = c0 + wc * (TC / WC) + i * 16 + 4 * kq + r;
+                    if (row >= a.cout) continue;
+                    const int c = perm32_channel(row);
+                    const long long o = (long long)p * a.ldy + c;
+                    float t = acc[i][j][r];
+                    if (affine) t = t * a.scale[c] + a.shift[c];
+                    if (resid) t += DT<TO>::to_f(R[o]);
+                    if (leaky) t = t > 0.f ? t : t * a.slope;
+                    Y[o] = DT<TO>::from_f(t);
+                }
+            }
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
         const int c = c0 + wc * (TC / WC) + i * 16 + 4 * kq;
@@ -277,6 +298,23 @@ static void launch(const ConvArgs& a, bool k1, hipStream_t s) {
 
 template <typename T, typename TO> void launch_gemm2(const ConvArgs& a, bool k1, hipStream_t s);
 
+// out[R][k] = w[chan(R)][ci][kh][kw] with k = (kh*KW + kw)*cin_pad + ci, zeros elsewhere.
+template <typename T>
+__global__ void k_pack_conv(const float* __restrict__ w, int cout, int cin, int kh, int kw, int cin_pad, int kp,
+                            int perm, T* __restrict__ out) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (long long)cout * kp) return;
+    const int R = (int)(i / kp), k = (int)(i - (long long)R * kp);
+    const int co = perm ? perm32_channel(R) : R;
+    const int tap = k / cin_pad, ci = k - tap * cin_pad;
+    float v = 0.f;
+    if (tap < kh * kw && ci < cin) {
+        const int y = tap / kw, x = tap - y * kw;
+        v = w[(((long long)co * cin + ci) * kh + y) * kw + x];
+    }
+    out[i] = DT<T>::from_f(v);
+}
+
 // v2 (LDS-DMA) engine eligibility: 128-byte K-steps and 31-bit buffer offsets.
 static bool use_v2(const ConvArgs& a, int dtype) {
     static int forced = -1;
@@ -339,4 +377,22 @@ extern "C" int rr_conv2d_fused(const void* x, const void* w, const float* scale,
     else if (dtype == RR_F32 && out_dtype == RR_F32) dispatch<float, float>(a, k1, dtype, s);
     else return fail(RR_EINVAL, "rr_conv2d_fused: unsupported dtype pair");
     return check_launch("rr_conv2d_fused");
+}
+
+extern "C" int rr_pack_conv_weights(const float* w, int c_out, int c_in, int kh, int kw, int c_in_pad, int k_packed,
+                                    int perm32, void* out, int dtype, void* stream) {
+    if (c_out <= 0 || c_in <= 0 || c_in_pad < c_in || k_packed < kh * kw * c_in_pad)
+        return fail(RR_EINVAL, "rr_pack_conv_weights: bad shape");
+    if (perm32 && (c_out % 32)) return fail(RR_EINVAL, "rr_pack_conv_weights: perm32 needs c_out % 32 == 0");
+    const long long total = (long long)c_out * k_packed;
+    const unsigned blocks = (unsigned)((total + 255) / 256);
+    if (dtype == RR_BF16)
+        hipLaunchKernelGGL(k_pack_conv<bf16_t>, dim3(blocks), dim3(256), 0, as_stream(stream), w, c_out, c_in, kh, kw,
+                           c_in_pad, k_packed, perm32, (bf16_t*)out);
+    else if (dtype == RR_F32)
+        hipLaunchKernelGGL(k_pack_conv<float>, dim3(blocks), dim3(256), 0, as_stream(stream), w, c_out, c_in, kh, kw,
+                           c_in_pad, k_packed, perm32, (float*)out);
+    else
+        return fail(RR_EINVAL, "rr_pack_conv_weights: dtype");
+    return check_launch("rr_pack_conv_weights");
 }

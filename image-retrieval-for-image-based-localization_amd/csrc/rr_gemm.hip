@@ -18,24 +18,18 @@
 //     (never __syncthreads(), whose fence would drain the prefetch).
 #include "rr_internal.h"
 
+#include <cstdlib>
+
 namespace rr {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;
-typedef __attribute__((address_space(3))) void lds_void;
 
 template <typename T> struct Vec2;
 template <> struct Vec2<bf16_t> { static constexpr int N = 8; };
 template <> struct Vec2<float> { static constexpr int N = 4; };
 
 constexpr unsigned OOB = 0x80000000u;  // voffset beyond every buffer: reads as 0
-
-// s_waitcnt vmcnt(n) (gfx9 encoding: vmcnt[3:0] | expcnt[6:4]=7 | lgkmcnt[11:8]=15 | vmcnt[5:4]<<14)
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-    static_assert(N >= 0 && N < 64, "vmcnt range");
-    __builtin_amdgcn_s_waitcnt((N & 0xF) | (0x7 << 4) | (0xF << 8) | ((N >> 4) << 14));
-}
 
 // One 16-B-per-lane LDS-DMA wave-instruction: LDS[m0 + lane*16] = buf[voff].
 // Issued from inline asm so hipcc neither counts it nor inserts a blanket
@@ -95,8 +89,15 @@ template <> struct St4<bf16_t> {
     }
 };
 
-template <typename T, typename TO, int TC, int TP, int WC, int WP, bool K1>
-__global__ void __launch_bounds__(256, 2) k_gemm2(ConvArgs a) {
+// Persistent tile loop: block b walks tiles t = b, b + grid, ... as one
+// flattened stream of (tile, K-step) steps, so the LDS-DMA of the next tile's
+// first K-step is in flight while the current tile's epilogue runs.
+// PERM: weight rows are stored in the 32-row MFMA-interleaved order
+// (packed row g*32 + i*16 + 4*q + r  <->  channel g*32 + 8*q + 4*i + r), so a
+// lane's two accumulator fragments hold 8 CONSECUTIVE output channels:
+// one 16-B bf16 store / residual load per (fragment pair, pixel).
+template <typename T, typename TO, int TC, int TP, int WC, int WP, bool K1, bool PERM, int NS>
+__global__ void __launch_bounds__(256, (NS == 2 ? 2 : 1)) k_igemm(ConvArgs a, int tiles_p, int ntiles) {
     constexpr int VEC = Vec2<T>::N;
     constexpr int BK = 8 * VEC;               // elements per K-step (128 B per row)
     constexpr int ESZ = sizeof(T);
@@ -105,53 +106,63 @@ __global__ void __launch_bounds__(256, 2) k_gemm2(ConvArgs a) {
     constexpr int FM = TC / WC / 16, FN = TP / WP / 16;
     constexpr int STAGE = (TC + TP) * 128;
     static_assert(WC * WP == 4 && TC % 32 == 0 && TP % 32 == 0, "tile");
+    static_assert(!PERM || FM % 2 == 0, "PERM pairs fragments");
 
-    __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+    static_assert(NS >= 2 && NS <= 4 && (NS - 1) * NLD < 64, "stages");
+    __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wc = wave % WC, wp = wave / WC;
-    const int c0 = blockIdx.y * TC, p0 = blockIdx.x * TP;
     const int H = a.h, W = a.w_, Cin = a.cin;
-
-    // ---- buffer resources: A = this block's weight rows, B = whole input
-    const long long arows = (long long)min(TC, a.cout - c0);
-    const i32x4_t rsA = make_rsrc((const char*)a.w + (long long)c0 * a.kp * ESZ, (unsigned)(arows * a.kp * ESZ));
     const long long xbytes = (long long)a.n * H * W * Cin * ESZ;
     const i32x4_t rsB = make_rsrc(a.x, (unsigned)xbytes);
     const unsigned lds0 = (unsigned)(unsigned long long)smem;
-
-    // ---- per-lane DMA descriptors
     const int lrow = lane >> 3;                 // row within an 8-row wave-instruction
     const int lchunk = (lane & 7) ^ (lrow & 7); // logical chunk fetched by this lane (source swizzle)
-    unsigned a_off[NIA];
-#pragma unroll
-    for (int i = 0; i < NIA; ++i) {
-        const int row = (wave + 4 * i) * 8 + lrow;
-        a_off[i] = row < arows ? (unsigned)(((long long)row * a.kp + lchunk * VEC) * ESZ) : OOB;
-    }
-    int b_hi[NIB], b_wi[NIB];
-    unsigned b_base[NIB];  // element offset of the pixel's (img, hi0, wi0) origin, or OOB
-#pragma unroll
-    for (int i = 0; i < NIB; ++i) {
-        const int row = (wave + 4 * i) * 8 + lrow;
-        const int p = p0 + row;
-        if (p < a.P) {
-            const int img = p / (a.ho * a.wo);
-            const int rem = p - img * (a.ho * a.wo);
-            const int oh = rem / a.wo, ow = rem - oh * a.wo;
-            b_hi[i] = oh * a.stride - a.pad;
-            b_wi[i] = ow * a.stride - a.pad;
-            long long base = (long long)img * H * W * Cin;
-            if (K1) base += ((long long)b_hi[i] * W + b_wi[i]) * Cin + lchunk * VEC;
-            b_base[i] = (unsigned)base;
-        } else {
-            b_hi[i] = b_wi[i] = 0;
-            b_base[i] = OOB;
-        }
-    }
+    const int nk = a.kp / BK;
+    const int my_tiles = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+    const int total = my_tiles * nk;
 
-    auto issue = [&](int stage, int k0) {
+    // ---- issue-side state (tile whose K-steps are being fetched)
+    i32x4_t rsA;
+    unsigned a_off[NIA];
+    int b_hi[NIB], b_wi[NIB];
+    unsigned b_base[NIB];
+    int is_tile = 0, is_k = 0;
+
+    auto setup_tile = [&](int t) {
+        const int c0 = (t / tiles_p) * TC, p0 = (t % tiles_p) * TP;
+        const long long arows = (long long)min(TC, a.cout - c0);
+        rsA = make_rsrc((const char*)a.w + (long long)c0 * a.kp * ESZ, (unsigned)(arows * a.kp * ESZ));
+#pragma unroll
+        for (int i = 0; i < NIA; ++i) {
+            const int row = (wave + 4 * i) * 8 + lrow;
+            a_off[i] = row < arows ? (unsigned)(((long long)row * a.kp + lchunk * VEC) * ESZ) : OOB;
+        }
+#pragma unroll
+        for (int i = 0; i < NIB; ++i) {
+            const int row = (wave + 4 * i) * 8 + lrow;
+            const int p = p0 + row;
+            if (p < a.P) {
+                const int img = p / (a.ho * a.wo);
+                const int rem = p - img * (a.ho * a.wo);
+                const int oh = rem / a.wo, ow = rem - oh * a.wo;
+                b_hi[i] = oh * a.stride - a.pad;
+                b_wi[i] = ow * a.stride - a.pad;
+                long long base = (long long)img * H * W * Cin;
+                if (K1) base += ((long long)b_hi[i] * W + b_wi[i]) * Cin + lchunk * VEC;
+                b_base[i] = (unsigned)base;
+            } else {
+                b_hi[i] = b_wi[i] = 0;
+                b_base[i] = OOB;
+            }
+        }
+    };
+
+    auto issue = [&](int stage) {  // fetch step (is_tile, is_k) into `stage`, then advance
+        if (is_k == 0) setup_tile((int)blockIdx.x + is_tile * (int)gridDim.x);
+        const int k0 = is_k * BK;
         const unsigned As = lds0 + stage * STAGE;
         const unsigned Bs = As + TC * 128;
 #pragma unroll
@@ -176,6 +187,7 @@ __global__ void __launch_bounds__(256, 2) k_gemm2(ConvArgs a) {
             }
             dma16(rsB, off, Bs + (wave + 4 * i) * 1024);
         }
+        if (++is_k == nk) { is_k = 0; ++is_tile; }
     };
 
     f32x4_t acc[FM][FN];
@@ -186,26 +198,177 @@ __global__ void __launch_bounds__(256, 2) k_gemm2(ConvArgs a) {
 
     const int r16 = lane & 15, kq = lane >> 4;
     const int arow0 = wc * (TC / WC) + r16, brow0 = wp * (TP / WP) + r16;
-    const int nk = a.kp / BK;
+    TO* __restrict__ Y = (TO*)a.y;
+    const TO* __restrict__ R = (const TO*)a.res;
+    const bool affine = a.flags & RR_CONV_AFFINE;
+    const bool resid = a.flags & RR_CONV_RESIDUAL;
+    const bool leaky = a.act == RR_ACT_LEAKY;
 
-    issue(0, 0);
-    for (int kt = 0; kt < nk; ++kt) {
-        const int cur = kt & 1;
-        if (kt + 1 < nk) {
-            issue(cur ^ 1, (kt + 1) * BK);
-            wait_vm_barrier<NLD>();   // this wave's stage-kt DMA done; barrier: everyone's
-        } else {
-            wait_vm_barrier<0>();
+    // bf16 PERM epilogue: the residual rows of the tile (8 channels = 16 B per
+    // (fragment pair, pixel)) are fetched into registers while the tile's last
+    // K-step is still on the MFMAs, so the epilogue does not wait on HBM.
+    constexpr bool PREF = PERM && sizeof(TO) == 2;
+    uint4 rres[PREF ? FM / 2 : 1][PREF ? FN : 1];
+    auto prefetch_res = [&](int t) {
+        if constexpr (PREF) {
+            if (!resid) return;
+            const int c0 = (t / tiles_p) * TC, p0 = (t % tiles_p) * TP;
+#pragma unroll
+            for (int i2 = 0; i2 < FM / 2; ++i2)
+#pragma unroll
+                for (int j = 0; j < FN; ++j) {
+                    const int c = c0 + wc * (TC / WC) + 32 * i2 + 8 * kq;
+                    const int p = p0 + wp * (TP / WP) + j * 16 + r16;
+                    rres[i2][j] = (c < a.cout && p < a.P)
+                                      ? *reinterpret_cast<const uint4*>(R + (long long)p * a.ldy + c)
+                                      : make_uint4(0, 0, 0, 0);
+                }
         }
+    };
+
+    auto epilogue = [&](int t) {
+        const int c0 = (t / tiles_p) * TC, p0 = (t % tiles_p) * TP;
+        if constexpr (PERM) {
+            float sc[FM / 2][8], sh[FM / 2][8];
+#pragma unroll
+            for (int i2 = 0; i2 < FM / 2; ++i2) {
+                const int c = min(c0 + wc * (TC / WC) + 32 * i2 + 8 * kq, a.cout - 8);
+                if (affine) {
+                    St4<float>::ld(a.scale + c, sc[i2]);
+                    St4<float>::ld(a.scale + c + 4, sc[i2] + 4);
+                    St4<float>::ld(a.shift + c, sh[i2]);
+                    St4<float>::ld(a.shift + c + 4, sh[i2] + 4);
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) { sc[i2][r] = 1.f; sh[i2][r] = 0.f; }
+                }
+            }
+#pragma unroll
+            for (int i2 = 0; i2 < FM / 2; ++i2) {
+                const int c = c0 + wc * (TC / WC) + 32 * i2 + 8 * kq;  // 8 consecutive channels
+                if (c >= a.cout) continue;                             // cout % 32 == 0 under PERM
+#pragma unroll
+                for (int j = 0; j < FN; ++j) {
+                    const int p = p0 + wp * (TP / WP) + j * 16 + r16;
+                    if (p >= a.P) continue;
+                    float v[8];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        v[r] = acc[2 * i2][j][r] * sc[i2][r] + sh[i2][r];
+                        v[4 + r] = acc[2 * i2 + 1][j][r] * sc[i2][4 + r] + sh[i2][4 + r];
+                    }
+                    const long long o = (long long)p * a.ldy + c;
+                    if (resid) {
+                        float rv[8];
+                        if constexpr (PREF) {
+                            const uint4 q = rres[i2][j];
+                            const unsigned w4[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                rv[2 * r] = __uint_as_float(w4[r] << 16);
+                                rv[2 * r + 1] = __uint_as_float(w4[r] & 0xffff0000u);
+                            }
+                        } else {
+                            St4<TO>::ld(R + o, rv);
+                            St4<TO>::ld(R + o + 4, rv + 4);
+                        }
+#pragma unroll
+                        for (int r = 0; r < 8; ++r) v[r] += rv[r];
+                    }
+                    if (leaky) {
+#pragma unroll
+                        for (int r = 0; r < 8; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * a.slope;
+                    }
+                    if constexpr (sizeof(TO) == 2) {
+                        uint4 q;
+                        q.x = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
+                        q.y = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+                        q.z = (unsigned)f2bf(v[4]) | ((unsigned)f2bf(v[5]) << 16);
+                        q.w = (unsigned)f2bf(v[6]) | ((unsigned)f2bf(v[7]) << 16);
+                        *reinterpret_cast<uint4*>(Y + o) = q;
+                    } else {
+                        St4<TO>::st(Y + o, v);
+                        St4<TO>::st(Y + o + 4, v + 4);
+                    }
+                }
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < FM; ++i) {
+                const int c = c0 + wc * (TC / WC) + i * 16 + 4 * kq;
+                if (c >= a.cout) continue;
+                float sc[4] = {1.f, 1.f, 1.f, 1.f}, sh[4] = {0.f, 0.f, 0.f, 0.f};
+                const bool full = (c + 3 < a.cout);
+                if (affine) {
+                    if (full) {
+                        St4<float>::ld(a.scale + c, sc);
+                        St4<float>::ld(a.shift + c, sh);
+                    } else {
+                        for (int r = 0; r < 4; ++r)
+                            if (c + r < a.cout) { sc[r] = a.scale[c + r]; sh[r] = a.shift[c + r]; }
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < FN; ++j) {
+                    const int p = p0 + wp * (TP / WP) + j * 16 + r16;
+                    if (p >= a.P) continue;
+                    float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+                    const long long o = (long long)p * a.ldy + c;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = v[r] * sc[r] + sh[r];
+                    if (full) {
+                        if (resid) {
+                            float rv[4];
+                            St4<TO>::ld(R + o, rv);
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) v[r] += rv[r];
+                        }
+                        if (leaky) {
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * a.slope;
+                        }
+                        St4<TO>::st(Y + o, v);
+                    } else {
+                        for (int r = 0; r < 4; ++r) {
+                            if (c + r >= a.cout) break;
+                            float tt = v[r];
+                            if (resid) tt += DT<TO>::to_f(R[o + r]);
+                            if (leaky) tt = tt > 0.f ? tt : tt * a.slope;
+                            Y[o + r] = DT<TO>::from_f(tt);
+                        }
+                    }
+                }
+            }
+        }
+    };
+
+    if (total == 0) return;
+    // NS-stage ring: steps s+1 .. s+NS-1 are in flight while step s computes.
+    int issued = 0;
+#pragma unroll
+    for (int i = 0; i < NS - 1; ++i)
+        if (issued < total) issue(issued++ % NS);
+    int ck = 0, ctile = 0;
+    for (int s = 0; s < total; ++s) {
+        const int cur = s % NS;
+        if (issued < total) issue(issued++ % NS);
+        // wait until this wave's step-s DMA is done (younger steps may stay in
+        // flight; older epilogue VMEM ops are drained too), then barrier: everyone's.
+        const int ahead = issued - s - 1;
+        if (NS >= 4 && ahead >= 3) wait_vm_barrier<(NS >= 4 ? 3 : 0) * NLD>();
+        else if (NS >= 3 && ahead == 2) wait_vm_barrier<(NS >= 3 ? 2 : 0) * NLD>();
+        else if (ahead == 1) wait_vm_barrier<NLD>();
+        else wait_vm_barrier<0>();
+        if (ck == nk - 1) prefetch_res((int)blockIdx.x + ctile * (int)gridDim.x);
         const char* As = smem + cur * STAGE;
         const char* Bs = As + TC * 128;
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
+        for (int hs = 0; hs < 2; ++hs) {
             uint4 fa[FM], fb[FN];
 #pragma unroll
-            for (int i = 0; i < FM; ++i) fa[i] = *reinterpret_cast<const uint4*>(As + swz(arow0 + i * 16, kq + 4 * s));
+            for (int i = 0; i < FM; ++i) fa[i] = *reinterpret_cast<const uint4*>(As + swz(arow0 + i * 16, kq + 4 * hs));
 #pragma unroll
-            for (int j = 0; j < FN; ++j) fb[j] = *reinterpret_cast<const uint4*>(Bs + swz(brow0 + j * 16, kq + 4 * s));
+            for (int j = 0; j < FN; ++j) fb[j] = *reinterpret_cast<const uint4*>(Bs + swz(brow0 + j * 16, kq + 4 * hs));
             if constexpr (VEC == 8) {
 #pragma unroll
                 for (int i = 0; i < FM; ++i)
@@ -229,81 +392,77 @@ __global__ void __launch_bounds__(256, 2) k_gemm2(ConvArgs a) {
             }
         }
         lds_barrier();  // every wave finished reading stage `cur` before it is refilled
-    }
-
-    // ---- fused epilogue (4 consecutive channels of one pixel per lane)
-    TO* __restrict__ Y = (TO*)a.y;
-    const TO* __restrict__ R = (const TO*)a.res;
-    const bool affine = a.flags & RR_CONV_AFFINE;
-    const bool resid = a.flags & RR_CONV_RESIDUAL;
-    const bool leaky = a.act == RR_ACT_LEAKY;
+        if (++ck == nk) {
+            epilogue((int)blockIdx.x + ctile * (int)gridDim.x);
 #pragma unroll
-    for (int i = 0; i < FM; ++i) {
-        const int c = c0 + wc * (TC / WC) + i * 16 + 4 * kq;
-        if (c >= a.cout) continue;
-        float sc[4] = {1.f, 1.f, 1.f, 1.f}, sh[4] = {0.f, 0.f, 0.f, 0.f};
-        const bool full = (c + 3 < a.cout);
-        if (affine) {
-            if (full) {
-                St4<float>::ld(a.scale + c, sc);
-                St4<float>::ld(a.shift + c, sh);
-            } else {
-                for (int r = 0; r < 4; ++r)
-                    if (c + r < a.cout) { sc[r] = a.scale[c + r]; sh[r] = a.shift[c + r]; }
-            }
-        }
+            for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) {
-            const int p = p0 + wp * (TP / WP) + j * 16 + r16;
-            if (p >= a.P) continue;
-            float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-            const long long o = (long long)p * a.ldy + c;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = v[r] * sc[r] + sh[r];
-            if (full) {
-                if (resid) {
-                    float rv[4];
-                    St4<TO>::ld(R + o, rv);
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] += rv[r];
-                }
-                if (leaky) {
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * a.slope;
-                }
-                St4<TO>::st(Y + o, v);
-            } else {
-                for (int r = 0; r < 4; ++r) {
-                    if (c + r >= a.cout) break;
-                    float t = v[r];
-                    if (resid) t += DT<TO>::to_f(R[o + r]);
-                    if (leaky) t = t > 0.f ? t : t * a.slope;
-                    Y[o + r] = DT<TO>::from_f(t);
-                }
-            }
+                for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+            ck = 0;
+            ++ctile;
         }
     }
 }
 
+static int g_num_cus = 0;
+static int g_stages = 0;
+
+static int num_cus() {
+    if (g_num_cus == 0) {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+            g_num_cus = cus;
+        else
+            g_num_cus = 256;
+        const char* e = getenv("RR_GEMM_STAGES");
+        g_stages = (e && (e[0] == '3')) ? 3 : 2;
+    }
+    return g_num_cus;
+}
+
+template <typename T, typename TO, int TC, int TP, int WC, int WP, int NS>
+static void launch_ns(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
+    constexpr int LDS = NS * (TC + TP) * 128;
+    constexpr int PER_CU = (160 * 1024) / LDS >= 2 ? 2 : 1;
+    const int tiles_p = (a.P + TP - 1) / TP;
+    const int tiles_c = (a.cout + TC - 1) / TC;
+    const int ntiles = tiles_p * tiles_c;
+    const int cap = PER_CU * num_cus();
+    const int grid = ntiles < cap ? ntiles : cap;
+#define RR_L3(K1V, PV) \
+    hipLaunchKernelGGL((k_igemm<T, TO, TC, TP, WC, WP, K1V, PV, NS>), dim3(grid), dim3(256), 0, s, a, tiles_p, ntiles)
+    if constexpr (sizeof(T) == sizeof(TO) && (TC / WC / 16) % 2 == 0) {
+        if (perm) {
+            if (k1) RR_L3(true, true); else RR_L3(false, true);
+            return;
+        }
+    }
+    if (k1) RR_L3(true, false); else RR_L3(false, false);
+#undef RR_L3
+}
+
 template <typename T, typename TO, int TC, int TP, int WC, int WP>
-static void launch2_cfg(const ConvArgs& a, bool k1, hipStream_t s) {
-    dim3 grid((a.P + TP - 1) / TP, (a.cout + TC - 1) / TC);
-    if (k1)
-        hipLaunchKernelGGL((k_gemm2<T, TO, TC, TP, WC, WP, true>), grid, dim3(256), 0, s, a);
-    else
-        hipLaunchKernelGGL((k_gemm2<T, TO, TC, TP, WC, WP, false>), grid, dim3(256), 0, s, a);
+static void launch_cfg3(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
+    num_cus();
+    if (g_stages == 3 && (3 * (TC + TP) * 128) <= 160 * 1024) launch_ns<T, TO, TC, TP, WC, WP, 3>(a, k1, perm, s);
+    else launch_ns<T, TO, TC, TP, WC, WP, 2>(a, k1, perm, s);
 }
 
 template <typename T, typename TO>
 void launch_gemm2(const ConvArgs& a, bool k1, hipStream_t s) {
+    const bool perm = (a.flags & RR_CONV_PERM32) != 0;
+    const int cus = num_cus();
     if (a.P <= 32)
-        launch2_cfg<T, TO, 256, 32, 4, 1>(a, k1, s);
+        launch_cfg3<T, TO, 256, 32, 4, 1>(a, k1, perm, s);
     else if (a.P <= 64)
-        launch2_cfg<T, TO, 256, 64, 4, 1>(a, k1, s);
+        launch_cfg3<T, TO, 256, 64, 4, 1>(a, k1, perm, s);
     else if (a.cout <= 64)
-        launch2_cfg<T, TO, 64, 256, 1, 4>(a, k1, s);
+        launch_cfg3<T, TO, 64, 256, 1, 4>(a, k1, perm, s);
+    else if ((long long)((a.P + 127) / 128) * ((a.cout + 127) / 128) < 2ll * cus)
+        launch_cfg3<T, TO, 64, 128, 1, 4>(a, k1, perm, s);   // too few 128x128 tiles to fill the chip
     else
-        launch2_cfg<T, TO, 128, 128, 2, 2>(a, k1, s);
+        launch_cfg3<T, TO, 128, 128, 2, 2>(a, k1, perm, s);
 }
 
 template void launch_gemm2<bf16_t, bf16_t>(const ConvArgs&, bool, hipStream_t);

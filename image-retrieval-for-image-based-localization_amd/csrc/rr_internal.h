@@ -68,6 +68,11 @@ struct ConvArgs {
 // scores[p][c] (f32, row stride ldy) = x[p][:] . w[c][:], 1x1 GEMM, dtype in.
 void gemm_scores(const ConvArgs& a, int dtype, hipStream_t s);
 
+// RR_CONV_PERM32 row order: packed row g*32 + i*16 + 4q + r holds channel g*32 + 8q + 4i + r.
+__host__ __device__ __forceinline__ int perm32_channel(int packed_row) {
+    return (packed_row & ~31) | (((packed_row & 15) >> 2) << 3) | (((packed_row >> 4) & 1) << 2) | (packed_row & 3);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -30,7 +30,7 @@ extern "C" {
 enum rr_dtype { RR_F32 = 0, RR_BF16 = 1 };
 enum rr_act { RR_ACT_IDENTITY = 0, RR_ACT_LEAKY = 1 };
 enum rr_pool_mode { RR_POOL_GEM = 0, RR_POOL_MAC = 1, RR_POOL_SPOC = 2 };
-enum rr_conv_flags { RR_CONV_AFFINE = 1, RR_CONV_RESIDUAL = 2 };
+enum rr_conv_flags { RR_CONV_AFFINE = 1, RR_CONV_RESIDUAL = 2, RR_CONV_PERM32 = 4 };
 enum rr_layout { RR_NHWC = 0, RR_NCHW = 1 };
 
 #define RR_OK 0
@@ -65,6 +65,9 @@ int rr_image_to_nhwc(const float* src, int n, int c, int h, int w,
  *   w  : [c_out][k_packed]          (dtype) k = (kh*KW + kw)*c_in + ci, zero padded
  *   y  : [n*ho*wo][ldy]             (out_dtype), channel c at column c
  *   residual : same layout/dtype as y (flag RR_CONV_RESIDUAL)
+ *   RR_CONV_PERM32: w rows are in the 32-row MFMA-interleaved order written by
+ *   rr_pack_conv_weights(perm32=1) (c_out % 32 == 0); y is still in natural
+ *   channel order.  scale/shift are always indexed by the natural channel.
  * Also used as the score GEMM of the kNN (1x1, ldy = slab width). */
 typedef struct rr_conv_desc {
     int n, h, w, c_in;     /* input; c_in = channel stride, power of two */
@@ -80,6 +83,13 @@ typedef struct rr_conv_desc {
 int rr_conv2d_fused(const void* x, const void* w, const float* scale, const float* shift,
                     const void* residual, void* y, const rr_conv_desc* desc,
                     int dtype, int out_dtype, void* stream);
+
+/* Pack nn.Conv2d weights w[c_out][c_in][kh][kw] (float32, the reference
+ * state-dict layout, cirtorch/backbones/resnet.py:61) into the engine layout
+ * out[c_out][k_packed] (`dtype`), k = (kh*KW + kw)*c_in_pad + ci, zero padded
+ * channels and K tail; perm32 != 0 stores rows in the RR_CONV_PERM32 order. */
+int rr_pack_conv_weights(const float* w, int c_out, int c_in, int kh, int kw, int c_in_pad,
+                         int k_packed, int perm32, void* out, int dtype, void* stream);
 
 /* 3x3/s2/p1 style max pooling, NHWC.  Replaces nn.MaxPool2d(3, stride=2,
  * padding=1) of the stem (cirtorch/backbones/resnet.py:65). */

@@ -34,7 +34,8 @@ CONV_CASES = [
 
 @pytest.mark.parametrize("case", CONV_CASES)
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
-def test_conv_fused(cuda, case, prec):
+@pytest.mark.parametrize("perm", [False, True])
+def test_conv_fused(cuda, case, prec, perm):
     n, cin, h, w, cout, k, s, p, use_res, leaky = case
     g = torch.Generator().manual_seed(hash(case) & 0xFFFF)
     x = torch.randn(n, cin, h, w, generator=g)
@@ -56,12 +57,20 @@ def test_conv_fused(cuda, case, prec):
         ref = F.leaky_relu(ref, 0.01)
     # engine layout
     cpad = cin if cin >= 8 else (8 if prec == "bf16" else 4)
+    perm = perm and cout % 32 == 0
     xe = F.pad(x.permute(0, 2, 3, 1), (0, cpad - cin)).contiguous().to(dtype).to(cuda)
-    wp = F.pad(wt.permute(0, 2, 3, 1), (0, cpad - cin)).reshape(cout, -1)
-    kp = (wp.shape[1] + 63) // 64 * 64
-    wp = F.pad(wp, (0, kp - wp.shape[1])).to(dtype).contiguous().to(cuda)
+    wp = _ops().pack_conv_weights(wt.to(cuda), cpad, dtype, perm32=perm)
+    # host check of the packed layout (k = (kh*KW + kw)*cin_pad + ci; perm32 row order)
+    ref_w = F.pad(wt.permute(0, 2, 3, 1), (0, cpad - cin)).reshape(cout, -1)
+    ref_w = F.pad(ref_w, (0, wp.shape[1] - ref_w.shape[1])).to(dtype)
+    if perm:
+        rows = torch.arange(cout)
+        chan = (rows & ~31) | (((rows & 15) >> 2) << 3) | (((rows >> 4) & 1) << 2) | (rows & 3)
+        ref_w = ref_w[chan]
+    assert torch.equal(wp.cpu(), ref_w)
     re = res.permute(0, 2, 3, 1).contiguous().to(dtype).to(cuda) if use_res else None
-    y = _ops().conv2d_fused(xe, wp, k, k, s, p, cout, scale.to(cuda), shift.to(cuda), residual=re, leaky=leaky)
+    y = _ops().conv2d_fused(xe, wp, k, k, s, p, cout, scale.to(cuda), shift.to(cuda), residual=re, leaky=leaky,
+                            perm32=perm)
     got = y.float().permute(0, 3, 1, 2).cpu().double()
     assert got.shape == ref.shape
     err = (got - ref).abs().max().item()
