@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=8, help="images per rank per step")
+    ap.add_argument("--batch", type=int, default=32, help="images per rank per step")
     ap.add_argument("--height", type=int, default=768)
     ap.add_argument("--width", type=int, default=1024)
     ap.add_argument("--arch", default="resnet50")

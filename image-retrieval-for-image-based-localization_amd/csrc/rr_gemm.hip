@@ -19,6 +19,7 @@
 #include "rr_internal.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace rr {
 
@@ -38,6 +39,7 @@ constexpr unsigned OOB = 0x80000000u;  // voffset beyond every buffer: reads as 
 typedef __attribute__((ext_vector_type(4))) int i32x4_t;
 __device__ __forceinline__ void dma16(i32x4_t rsrc, unsigned voff, unsigned lds_addr) {
     unsigned keep;
+    lds_addr = __builtin_amdgcn_readfirstlane(lds_addr);  // wave-uniform by construction; make it provable
     asm volatile(
         "s_mov_b32 %0, m0\n\t"
         "s_mov_b32 m0, %3\n\t"
@@ -97,15 +99,16 @@ template <> struct St4<bf16_t> {
 // lane's two accumulator fragments hold 8 CONSECUTIVE output channels:
 // one 16-B bf16 store / residual load per (fragment pair, pixel).
 template <typename T, typename TO, int TC, int TP, int WC, int WP, bool K1, bool PERM, int NS>
-__global__ void __launch_bounds__(256, (NS == 2 ? 2 : 1)) k_igemm(ConvArgs a, int tiles_p, int ntiles) {
+__global__ void __launch_bounds__(64 * WC * WP, (NS == 2 || WC * WP == 8 ? 2 : 1)) k_igemm(ConvArgs a, int tiles_p, int ntiles) {
     constexpr int VEC = Vec2<T>::N;
     constexpr int BK = 8 * VEC;               // elements per K-step (128 B per row)
     constexpr int ESZ = sizeof(T);
-    constexpr int NIA = TC / 32, NIB = TP / 32;  // LDS-DMA instructions per wave per stage
+    constexpr int NW = WC * WP;                  // waves per block (4 or 8)
+    constexpr int NIA = TC / (8 * NW), NIB = TP / (8 * NW);  // LDS-DMA instructions per wave per stage
     constexpr int NLD = NIA + NIB;
     constexpr int FM = TC / WC / 16, FN = TP / WP / 16;
     constexpr int STAGE = (TC + TP) * 128;
-    static_assert(WC * WP == 4 && TC % 32 == 0 && TP % 32 == 0, "tile");
+    static_assert((NW == 4 || NW == 8) && TC % (8 * NW) == 0 && TP % (8 * NW) == 0, "tile");
     static_assert(!PERM || FM % 2 == 0, "PERM pairs fragments");
 
     static_assert(NS >= 2 && NS <= 4 && (NS - 1) * NLD < 64, "stages");
@@ -137,12 +140,12 @@ __global__ void __launch_bounds__(256, (NS == 2 ? 2 : 1)) k_igemm(ConvArgs a, in
         rsA = make_rsrc((const char*)a.w + (long long)c0 * a.kp * ESZ, (unsigned)(arows * a.kp * ESZ));
 #pragma unroll
         for (int i = 0; i < NIA; ++i) {
-            const int row = (wave + 4 * i) * 8 + lrow;
+            const int row = (wave + NW * i) * 8 + lrow;
             a_off[i] = row < arows ? (unsigned)(((long long)row * a.kp + lchunk * VEC) * ESZ) : OOB;
         }
 #pragma unroll
         for (int i = 0; i < NIB; ++i) {
-            const int row = (wave + 4 * i) * 8 + lrow;
+            const int row = (wave + NW * i) * 8 + lrow;
             const int p = p0 + row;
             if (p < a.P) {
                 const int img = p / (a.ho * a.wo);
@@ -168,7 +171,7 @@ __global__ void __launch_bounds__(256, (NS == 2 ? 2 : 1)) k_igemm(ConvArgs a, in
 #pragma unroll
         for (int i = 0; i < NIA; ++i) {
             const unsigned off = a_off[i] == OOB ? OOB : a_off[i] + (unsigned)(k0 * ESZ);
-            dma16(rsA, off, As + (wave + 4 * i) * 1024);
+            dma16(rsA, off, As + (wave + NW * i) * 1024);
         }
 #pragma unroll
         for (int i = 0; i < NIB; ++i) {
@@ -185,7 +188,7 @@ __global__ void __launch_bounds__(256, (NS == 2 ? 2 : 1)) k_igemm(ConvArgs a, in
                 const bool ok = b_base[i] != OOB && kh < a.kh && hi >= 0 && hi < H && wi >= 0 && wi < W;
                 off = ok ? (unsigned)((b_base[i] + ((long long)hi * W + wi) * Cin + ci) * ESZ) : OOB;
             }
-            dma16(rsB, off, Bs + (wave + 4 * i) * 1024);
+            dma16(rsB, off, Bs + (wave + NW * i) * 1024);
         }
         if (++is_k == nk) { is_k = 0; ++is_tile; }
     };
@@ -207,9 +210,15 @@ __global__ void __launch_bounds__(256, (NS == 2 ? 2 : 1)) k_igemm(ConvArgs a, in
     // bf16 PERM epilogue: the residual rows of the tile (8 channels = 16 B per
     // (fragment pair, pixel)) are fetched into registers while the tile's last
     // K-step is still on the MFMAs, so the epilogue does not wait on HBM.
-    constexpr bool PREF = PERM && sizeof(TO) == 2;
-    uint4 rres[PREF ? FM / 2 : 1][PREF ? FN : 1];
-    auto prefetch_res = [&](int t) {
+    // With a 2-stage ring (XPREF) the fetch is issued one tile ahead, together
+    // with that tile's first LDS-DMA, into the other of two register buffers,
+    // so even single-K-step (K = 64) layers overlap the residual read.
+    // (residual convs are the 1x1 conv3 of a block: K1 only; register budget: no spills at 64x64/wave)
+    constexpr bool PREF = PERM && K1 && sizeof(TO) == 2 && FM * FN <= 16;
+    constexpr bool XPREF = PREF && NS == 2;
+    uint4 rres[XPREF ? 2 : 1][PREF ? FM / 2 : 1][PREF ? FN : 1];
+    auto prefetch_res = [&](auto bsel, int t) {
+        constexpr int BUF = decltype(bsel)::value;
         if constexpr (PREF) {
             if (!resid) return;
             const int c0 = (t / tiles_p) * TC, p0 = (t % tiles_p) * TP;
@@ -219,14 +228,15 @@ __global__ void __launch_bounds__(256, (NS == 2 ? 2 : 1)) k_igemm(ConvArgs a, in
                 for (int j = 0; j < FN; ++j) {
                     const int c = c0 + wc * (TC / WC) + 32 * i2 + 8 * kq;
                     const int p = p0 + wp * (TP / WP) + j * 16 + r16;
-                    rres[i2][j] = (c < a.cout && p < a.P)
+                    rres[BUF][i2][j] = (c < a.cout && p < a.P)
                                       ? *reinterpret_cast<const uint4*>(R + (long long)p * a.ldy + c)
                                       : make_uint4(0, 0, 0, 0);
                 }
         }
     };
 
-    auto epilogue = [&](int t) {
+    auto epilogue = [&](auto bsel, int t) {
+        constexpr int BUF = decltype(bsel)::value;
         const int c0 = (t / tiles_p) * TC, p0 = (t % tiles_p) * TP;
         if constexpr (PERM) {
             float sc[FM / 2][8], sh[FM / 2][8];
@@ -261,7 +271,7 @@ __global__ void __launch_bounds__(256, (NS == 2 ? 2 : 1)) k_igemm(ConvArgs a, in
                     if (resid) {
                         float rv[8];
                         if constexpr (PREF) {
-                            const uint4 q = rres[i2][j];
+                            const uint4 q = rres[BUF][i2][j];
                             const unsigned w4[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
                             for (int r = 0; r < 4; ++r) {
@@ -344,14 +354,26 @@ __global__ void __launch_bounds__(256, (NS == 2 ? 2 : 1)) k_igemm(ConvArgs a, in
 
     if (total == 0) return;
     // NS-stage ring: steps s+1 .. s+NS-1 are in flight while step s computes.
+    using B0 = std::integral_constant<int, 0>;
+    using B1 = std::integral_constant<int, 1>;
+    auto xprefetch = [&]() {  // after issue(): the issued step opened tile `is_tile - 1`
+        if constexpr (XPREF) {
+            if (is_k == 1 % nk || nk == 1) {
+                const int lt = is_k == 0 ? is_tile - 1 : is_tile;  // local index of the tile just opened
+                const int t = (int)blockIdx.x + lt * (int)gridDim.x;
+                if (lt & 1) prefetch_res(B1{}, t);
+                else prefetch_res(B0{}, t);
+            }
+        }
+    };
     int issued = 0;
 #pragma unroll
     for (int i = 0; i < NS - 1; ++i)
-        if (issued < total) issue(issued++ % NS);
+        if (issued < total) { issue(issued++ % NS); xprefetch(); }
     int ck = 0, ctile = 0;
     for (int s = 0; s < total; ++s) {
         const int cur = s % NS;
-        if (issued < total) issue(issued++ % NS);
+        if (issued < total) { issue(issued++ % NS); xprefetch(); }
         // wait until this wave's step-s DMA is done (younger steps may stay in
         // flight; older epilogue VMEM ops are drained too), then barrier: everyone's.
         const int ahead = issued - s - 1;
@@ -359,7 +381,9 @@ __global__ void __launch_bounds__(256, (NS == 2 ? 2 : 1)) k_igemm(ConvArgs a, in
         else if (NS >= 3 && ahead == 2) wait_vm_barrier<(NS >= 3 ? 2 : 0) * NLD>();
         else if (ahead == 1) wait_vm_barrier<NLD>();
         else wait_vm_barrier<0>();
-        if (ck == nk - 1) prefetch_res((int)blockIdx.x + ctile * (int)gridDim.x);
+        if constexpr (!XPREF) {
+            if (ck == nk - 1) prefetch_res(B0{}, (int)blockIdx.x + ctile * (int)gridDim.x);
+        }
         const char* As = smem + cur * STAGE;
         const char* Bs = As + TC * 128;
 #pragma unroll
@@ -393,7 +417,13 @@ __global__ void __launch_bounds__(256, (NS == 2 ? 2 : 1)) k_igemm(ConvArgs a, in
         }
         lds_barrier();  // every wave finished reading stage `cur` before it is refilled
         if (++ck == nk) {
-            epilogue((int)blockIdx.x + ctile * (int)gridDim.x);
+            const int t = (int)blockIdx.x + ctile * (int)gridDim.x;
+            if constexpr (XPREF) {
+                if (ctile & 1) epilogue(B1{}, t);
+                else epilogue(B0{}, t);
+            } else {
+                epilogue(B0{}, t);
+            }
 #pragma unroll
             for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -406,6 +436,7 @@ __global__ void __launch_bounds__(256, (NS == 2 ? 2 : 1)) k_igemm(ConvArgs a, in
 
 static int g_num_cus = 0;
 static int g_stages = 0;
+static bool g_wide = true;
 
 static int num_cus() {
     if (g_num_cus == 0) {
@@ -417,6 +448,8 @@ static int num_cus() {
             g_num_cus = 256;
         const char* e = getenv("RR_GEMM_STAGES");
         g_stages = (e && (e[0] == '3')) ? 3 : 2;
+        const char* w = getenv("RR_GEMM_WIDE");
+        g_wide = !(w && w[0] == '0');
     }
     return g_num_cus;
 }
@@ -424,14 +457,14 @@ static int num_cus() {
 template <typename T, typename TO, int TC, int TP, int WC, int WP, int NS>
 static void launch_ns(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
     constexpr int LDS = NS * (TC + TP) * 128;
-    constexpr int PER_CU = (160 * 1024) / LDS >= 2 ? 2 : 1;
+    constexpr int PER_CU = ((160 * 1024) / LDS >= 2 && WC * WP == 4) ? 2 : 1;
     const int tiles_p = (a.P + TP - 1) / TP;
     const int tiles_c = (a.cout + TC - 1) / TC;
     const int ntiles = tiles_p * tiles_c;
     const int cap = PER_CU * num_cus();
     const int grid = ntiles < cap ? ntiles : cap;
 #define RR_L3(K1V, PV) \
-    hipLaunchKernelGGL((k_igemm<T, TO, TC, TP, WC, WP, K1V, PV, NS>), dim3(grid), dim3(256), 0, s, a, tiles_p, ntiles)
+    hipLaunchKernelGGL((k_igemm<T, TO, TC, TP, WC, WP, K1V, PV, NS>), dim3(grid), dim3(64 * WC * WP), 0, s, a, tiles_p, ntiles)
     if constexpr (sizeof(T) == sizeof(TO) && (TC / WC / 16) % 2 == 0) {
         if (perm) {
             if (k1) RR_L3(true, true); else RR_L3(false, true);
@@ -445,8 +478,13 @@ static void launch_ns(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
 template <typename T, typename TO, int TC, int TP, int WC, int WP>
 static void launch_cfg3(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
     num_cus();
-    if (g_stages == 3 && (3 * (TC + TP) * 128) <= 160 * 1024) launch_ns<T, TO, TC, TP, WC, WP, 3>(a, k1, perm, s);
-    else launch_ns<T, TO, TC, TP, WC, WP, 2>(a, k1, perm, s);
+    if constexpr (3 * (TC + TP) * 128 <= 160 * 1024 && WC * WP == 4) {
+        if (g_stages == 3) {
+            launch_ns<T, TO, TC, TP, WC, WP, 3>(a, k1, perm, s);
+            return;
+        }
+    }
+    launch_ns<T, TO, TC, TP, WC, WP, 2>(a, k1, perm, s);
 }
 
 template <typename T, typename TO>
@@ -459,8 +497,10 @@ void launch_gemm2(const ConvArgs& a, bool k1, hipStream_t s) {
         launch_cfg3<T, TO, 256, 64, 4, 1>(a, k1, perm, s);
     else if (a.cout <= 64)
         launch_cfg3<T, TO, 64, 256, 1, 4>(a, k1, perm, s);
-    else if ((long long)((a.P + 127) / 128) * ((a.cout + 127) / 128) < 2ll * cus)
-        launch_cfg3<T, TO, 64, 128, 1, 4>(a, k1, perm, s);   // too few 128x128 tiles to fill the chip
+    else if (g_wide && a.kp >= 512 && a.cout >= 256 && (long long)((a.P + 255) / 256) * ((a.cout + 255) / 256) >= cus)
+        launch_cfg3<T, TO, 256, 256, 4, 2>(a, k1, perm, s);   // 8 waves, 64x128 per wave
+    else if (g_wide && a.kp >= 512 && a.cout >= 256 && (long long)((a.P + 127) / 128) * ((a.cout + 255) / 256) >= cus)
+        launch_cfg3<T, TO, 256, 128, 4, 2>(a, k1, perm, s);   // 8 waves, 64x64 per wave
     else
         launch_cfg3<T, TO, 128, 128, 2, 2>(a, k1, perm, s);
 }
