@@ -44,6 +44,68 @@ __global__ void k_image_to_nhwc(const float* __restrict__ src, int n, int c, int
     }
 }
 
+// bf16, c = 3, c_pad = 8: one thread per pixel, one 16-B store; reads are
+// coalesced along w within each of the 3 planes.
+__global__ void k_image_to_nhwc_bf16x8(const float* __restrict__ src, long long npix, int hw, NormParams np,
+                                       int do_norm, uint4* __restrict__ dst) {
+    const long long pix = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (pix >= npix) return;
+    const long long img = pix / hw;
+    const long long off = pix - img * hw;
+    const float* s = src + img * 3 * hw + off;
+    float v[3];
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+        v[ch] = s[(long long)ch * hw];
+        if (do_norm) v[ch] = (v[ch] - np.mean[ch]) / np.stdv[ch];
+    }
+    uint4 o;
+    o.x = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
+    o.y = (unsigned)f2bf(v[2]);
+    o.z = 0u;
+    o.w = 0u;
+    dst[pix] = o;
+}
+
+// NHWC max-pool, 8 channels (16 B of bf16) per thread.
+__global__ void k_maxpool_nhwc_bf16x8(const uint4* __restrict__ x, int n, int h, int w, int c8, int k, int stride,
+                                      int pad, uint4* __restrict__ y, int ho, int wo) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long total = (long long)n * ho * wo * c8;
+    if (i >= total) return;
+    const int cc = (int)(i % c8);
+    long long r = i / c8;
+    const int ow = (int)(r % wo);
+    r /= wo;
+    const int oh = (int)(r % ho);
+    const int img = (int)(r / ho);
+    float m[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m[e] = -INFINITY;
+    const int h0 = oh * stride - pad, w0 = ow * stride - pad;
+    for (int a = 0; a < k; ++a) {
+        const int hh = h0 + a;
+        if (hh < 0 || hh >= h) continue;
+        for (int b = 0; b < k; ++b) {
+            const int ww = w0 + b;
+            if (ww < 0 || ww >= w) continue;
+            const uint4 q = x[(((long long)img * h + hh) * w + ww) * c8 + cc];
+            const unsigned u[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                m[2 * e] = fmaxf(m[2 * e], __uint_as_float(u[e] << 16));
+                m[2 * e + 1] = fmaxf(m[2 * e + 1], __uint_as_float(u[e] & 0xffff0000u));
+            }
+        }
+    }
+    uint4 o;
+    o.x = (unsigned)f2bf(m[0]) | ((unsigned)f2bf(m[1]) << 16);
+    o.y = (unsigned)f2bf(m[2]) | ((unsigned)f2bf(m[3]) << 16);
+    o.z = (unsigned)f2bf(m[4]) | ((unsigned)f2bf(m[5]) << 16);
+    o.w = (unsigned)f2bf(m[6]) | ((unsigned)f2bf(m[7]) << 16);
+    y[i] = o;
+}
+
 // ------------------------------------------------------------------ max-pool
 template <typename T>
 __global__ void k_maxpool_nhwc(const T* __restrict__ x, int n, int h, int w, int c, int k, int stride,
@@ -183,7 +245,10 @@ int rr_image_to_nhwc(const float* src, int n, int c, int h, int w, const float* 
         np.stdv[i] = do_normalize ? std_host[i] : 1.f;  // divisor (true division in kernel)
     }
     long long total = (long long)n * h * w;
-    if (dtype == RR_BF16)
+    if (dtype == RR_BF16 && c == 3 && c_pad == 8 && (((uintptr_t)dst) & 15) == 0)
+        hipLaunchKernelGGL(k_image_to_nhwc_bf16x8, dim3(nblk(total, 256)), dim3(256), 0, as_stream(stream), src,
+                           total, h * w, np, do_normalize, (uint4*)dst);
+    else if (dtype == RR_BF16)
         hipLaunchKernelGGL(k_image_to_nhwc<bf16_t>, dim3(nblk(total, 256)), dim3(256), 0, as_stream(stream), src, n,
                            c, h * w, np, do_normalize, (bf16_t*)dst, c_pad);
     else if (dtype == RR_F32)
@@ -198,7 +263,10 @@ int rr_maxpool2d(const void* x, int n, int h, int w, int c, int k, int stride, i
                  int dtype, void* stream) {
     long long total = (long long)n * ho * wo * c;
     if (total <= 0) return fail(RR_EINVAL, "rr_maxpool2d: empty");
-    if (dtype == RR_BF16)
+    if (dtype == RR_BF16 && c % 8 == 0 && (((uintptr_t)x | (uintptr_t)y) & 15) == 0)
+        hipLaunchKernelGGL(k_maxpool_nhwc_bf16x8, dim3(nblk(total / 8, 256)), dim3(256), 0, as_stream(stream),
+                           (const uint4*)x, n, h, w, c / 8, k, stride, pad, (uint4*)y, ho, wo);
+    else if (dtype == RR_BF16)
         hipLaunchKernelGGL(k_maxpool_nhwc<bf16_t>, dim3(nblk(total, 256)), dim3(256), 0, as_stream(stream),
                            (const bf16_t*)x, n, h, w, c, k, stride, pad, (bf16_t*)y, ho, wo);
     else if (dtype == RR_F32)

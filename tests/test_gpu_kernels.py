@@ -80,11 +80,24 @@ def test_conv_fused(cuda, case, prec, perm):
     assert err <= tol, (err, scale_ref)
 
 
-def test_maxpool(cuda):
-    x = torch.randn(2, 21, 19, 64)
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_maxpool(cuda, dtype):
+    x = torch.randn(2, 21, 19, 64).to(dtype)
     y = _ops().maxpool2d(x.to(cuda), 3, 2, 1).cpu()
-    ref = F.max_pool2d(x.permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
+    ref = F.max_pool2d(x.float().permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1).to(dtype)
     assert torch.equal(y, ref)
+
+
+@pytest.mark.parametrize("dtype,cpad", [(torch.float32, 4), (torch.bfloat16, 8)])
+def test_image_to_nhwc(cuda, dtype, cpad):
+    """normalise (cirtorch/utils/image.py:125) + NCHW->NHWC + zero channel pad."""
+    x = torch.rand(2, 3, 13, 17)
+    mean, std = [0.485, 0.456, 0.406], [0.229, 0.224, 0.225]
+    y = _ops().image_to_nhwc(x.to(cuda), cpad, dtype, mean, std).cpu()
+    ref = ((x - torch.tensor(mean)[:, None, None]) / torch.tensor(std)[:, None, None]).permute(0, 2, 3, 1)
+    assert y.shape == (2, 13, 17, cpad)
+    assert torch.equal(y[..., :3], ref.to(dtype))
+    assert y[..., 3:].abs().sum() == 0
 
 
 def test_resize_bilinear(cuda):
