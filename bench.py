@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--knn-q", type=int, default=1024, help="queries for the kNN-only sub-benchmark (0 = skip)")
     ap.add_argument("--knn-steps", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--overlap", action="store_true",
+                    help="run batch i's match on a second stream, overlapping batch i+1's extract (measured slower on one GPU)")
     ap.add_argument("--cpu-images", type=int, default=2)
     ap.add_argument("--cpu-db-rows", type=int, default=100_000)
     return ap.parse_args()
@@ -147,21 +149,36 @@ def main():
 
     ev_pairs = []
 
-    def step(record):
-        e0 = e1 = None
-        if record:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-        desc = net.extract(images)                  # D x B (on-device, fp32)
-        if record:
-            e1.record()
-            ev_pairs.append((e0, e1))
+    main_stream = torch.cuda.current_stream(dev)
+    match_stream = torch.cuda.Stream(dev) if args.overlap else main_stream
+
+    def match(desc):
         q = desc.t().contiguous()
         if world > 1:
             qa = torch.empty((world * B, q.shape[1]), dtype=q.dtype, device=dev)
             dist.all_gather_into_tensor(qa, q)
             q = qa
         return index.search(q, args.k)
+
+    def step(record):
+        """extract batch i on the main stream; its match (memory-bound kNN +
+        RCCL) runs on a second stream, overlapping batch i+1's extraction."""
+        e0 = e1 = None
+        if record:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(main_stream)
+        desc = net.extract(images)                  # D x B (on-device, fp32)
+        if record:
+            e1.record(main_stream)
+            ev_pairs.append((e0, e1))
+        if match_stream is main_stream:
+            return match(desc)
+        ready = torch.cuda.Event()
+        ready.record(main_stream)
+        with torch.cuda.stream(match_stream):
+            match_stream.wait_event(ready)
+            desc.record_stream(match_stream)
+            return match(desc)
 
     with torch.no_grad():
         for _ in range(args.warmup):

@@ -396,3 +396,12 @@ extern "C" int rr_pack_conv_weights(const float* w, int c_out, int c_in, int kh,
         return fail(RR_EINVAL, "rr_pack_conv_weights: dtype");
     return check_launch("rr_pack_conv_weights");
 }
+
+namespace rr {
+void set_gemm_tuning(int key, int value);
+}
+extern "C" int rr_set_tuning(int key, int value) {
+    if (key < 0 || key > 3) return fail(RR_EINVAL, "rr_set_tuning: unknown key");
+    rr::set_gemm_tuning(key, value);
+    return RR_OK;
+}

@@ -98,8 +98,12 @@ template <> struct St4<bf16_t> {
 // (packed row g*32 + i*16 + 4*q + r  <->  channel g*32 + 8*q + 4*i + r), so a
 // lane's two accumulator fragments hold 8 CONSECUTIVE output channels:
 // one 16-B bf16 store / residual load per (fragment pair, pixel).
-template <typename T, typename TO, int TC, int TP, int WC, int WP, bool K1, bool PERM, int NS>
-__global__ void __launch_bounds__(64 * WC * WP, (NS == 2 || WC * WP == 8 ? 2 : 1)) k_igemm(ConvArgs a, int tiles_p, int ntiles) {
+// AK > 0 ("A-stationary"): the layer has a single output-channel tile
+// (c_out <= TC) and at most AK K-steps, so the whole weight slice is fetched
+// into LDS once per block and only the activation tile streams through the
+// ring — the per-CU LDS-DMA volume drops to the B operand alone.
+template <typename T, typename TO, int TC, int TP, int WC, int WP, bool K1, bool PERM, int NS, int AK>
+__global__ void __launch_bounds__(64 * WC * WP, ((NS == 2 && AK * TC <= 256) || WC * WP == 8 ? 2 : 1)) k_igemm(ConvArgs a, int tiles_p, int ntiles) {
     constexpr int VEC = Vec2<T>::N;
     constexpr int BK = 8 * VEC;               // elements per K-step (128 B per row)
     constexpr int ESZ = sizeof(T);
@@ -107,12 +111,14 @@ __global__ void __launch_bounds__(64 * WC * WP, (NS == 2 || WC * WP == 8 ? 2 : 1
     constexpr int NIA = TC / (8 * NW), NIB = TP / (8 * NW);  // LDS-DMA instructions per wave per stage
     constexpr int NLD = NIA + NIB;
     constexpr int FM = TC / WC / 16, FN = TP / WP / 16;
-    constexpr int STAGE = (TC + TP) * 128;
+    constexpr int STAGE = (AK ? TP : TC + TP) * 128;
+    constexpr int ABYTES = AK * TC * 128;
+    static_assert(AK == 0 || NS == 2, "A-stationary uses the 2-stage ring");
     static_assert((NW == 4 || NW == 8) && TC % (8 * NW) == 0 && TP % (8 * NW) == 0, "tile");
     static_assert(!PERM || FM % 2 == 0, "PERM pairs fragments");
 
     static_assert(NS >= 2 && NS <= 4 && (NS - 1) * NLD < 64, "stages");
-    __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
+    __shared__ __attribute__((aligned(1024))) char smem[ABYTES + NS * STAGE];
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -167,11 +173,22 @@ __global__ void __launch_bounds__(64 * WC * WP, (NS == 2 || WC * WP == 8 ? 2 : 1
         if (is_k == 0) setup_tile((int)blockIdx.x + is_tile * (int)gridDim.x);
         const int k0 = is_k * BK;
         const unsigned As = lds0 + stage * STAGE;
-        const unsigned Bs = As + TC * 128;
+        const unsigned Bs = AK ? lds0 + ABYTES + stage * STAGE : As + TC * 128;
+        if constexpr (AK > 0) {
+            if (is_tile == 0 && is_k == 0) {  // whole weight slice, once per block
+                for (int kk = 0; kk < nk; ++kk)
 #pragma unroll
-        for (int i = 0; i < NIA; ++i) {
-            const unsigned off = a_off[i] == OOB ? OOB : a_off[i] + (unsigned)(k0 * ESZ);
-            dma16(rsA, off, As + (wave + NW * i) * 1024);
+                    for (int i = 0; i < NIA; ++i) {
+                        const unsigned off = a_off[i] == OOB ? OOB : a_off[i] + (unsigned)(kk * BK * ESZ);
+                        dma16(rsA, off, lds0 + kk * TC * 128 + (wave + NW * i) * 1024);
+                    }
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < NIA; ++i) {
+                const unsigned off = a_off[i] == OOB ? OOB : a_off[i] + (unsigned)(k0 * ESZ);
+                dma16(rsA, off, As + (wave + NW * i) * 1024);
+            }
         }
 #pragma unroll
         for (int i = 0; i < NIB; ++i) {
@@ -379,13 +396,13 @@ __global__ void __launch_bounds__(64 * WC * WP, (NS == 2 || WC * WP == 8 ? 2 : 1
         const int ahead = issued - s - 1;
         if (NS >= 4 && ahead >= 3) wait_vm_barrier<(NS >= 4 ? 3 : 0) * NLD>();
         else if (NS >= 3 && ahead == 2) wait_vm_barrier<(NS >= 3 ? 2 : 0) * NLD>();
-        else if (ahead == 1) wait_vm_barrier<NLD>();
+        else if (ahead == 1) wait_vm_barrier<AK ? NIB : NLD>();  // AK: a step issues B only (A's one-time load is older)
         else wait_vm_barrier<0>();
         if constexpr (!XPREF) {
             if (ck == nk - 1) prefetch_res(B0{}, (int)blockIdx.x + ctile * (int)gridDim.x);
         }
-        const char* As = smem + cur * STAGE;
-        const char* Bs = As + TC * 128;
+        const char* As = AK ? smem + ck * TC * 128 : smem + cur * STAGE;
+        const char* Bs = AK ? smem + ABYTES + cur * STAGE : As + TC * 128;
 #pragma unroll
         for (int hs = 0; hs < 2; ++hs) {
             uint4 fa[FM], fb[FN];
@@ -437,6 +454,7 @@ __global__ void __launch_bounds__(64 * WC * WP, (NS == 2 || WC * WP == 8 ? 2 : 1
 static int g_num_cus = 0;
 static int g_stages = 0;
 static bool g_wide = true;
+static bool g_ast = false;
 
 static int num_cus() {
     if (g_num_cus == 0) {
@@ -454,9 +472,9 @@ static int num_cus() {
     return g_num_cus;
 }
 
-template <typename T, typename TO, int TC, int TP, int WC, int WP, int NS>
+template <typename T, typename TO, int TC, int TP, int WC, int WP, int NS, int AK = 0>
 static void launch_ns(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
-    constexpr int LDS = NS * (TC + TP) * 128;
+    constexpr int LDS = AK * TC * 128 + NS * (AK ? TP : TC + TP) * 128;
     constexpr int PER_CU = ((160 * 1024) / LDS >= 2 && WC * WP == 4) ? 2 : 1;
     const int tiles_p = (a.P + TP - 1) / TP;
     const int tiles_c = (a.cout + TC - 1) / TC;
@@ -464,7 +482,7 @@ static void launch_ns(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
     const int cap = PER_CU * num_cus();
     const int grid = ntiles < cap ? ntiles : cap;
 #define RR_L3(K1V, PV) \
-    hipLaunchKernelGGL((k_igemm<T, TO, TC, TP, WC, WP, K1V, PV, NS>), dim3(grid), dim3(64 * WC * WP), 0, s, a, tiles_p, ntiles)
+    hipLaunchKernelGGL((k_igemm<T, TO, TC, TP, WC, WP, K1V, PV, NS, AK>), dim3(grid), dim3(64 * WC * WP), 0, s, a, tiles_p, ntiles)
     if constexpr (sizeof(T) == sizeof(TO) && (TC / WC / 16) % 2 == 0) {
         if (perm) {
             if (k1) RR_L3(true, true); else RR_L3(false, true);
@@ -487,10 +505,36 @@ static void launch_cfg3(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
     launch_ns<T, TO, TC, TP, WC, WP, 2>(a, k1, perm, s);
 }
 
+int g_force_cfg = 0;  // rr_set_tuning(RR_TUNE_GEMM_CONFIG, ...)
+
 template <typename T, typename TO>
 void launch_gemm2(const ConvArgs& a, bool k1, hipStream_t s) {
     const bool perm = (a.flags & RR_CONV_PERM32) != 0;
     const int cus = num_cus();
+    switch (g_force_cfg) {
+        case 1: launch_cfg3<T, TO, 128, 128, 2, 2>(a, k1, perm, s); return;
+        case 2: launch_cfg3<T, TO, 64, 256, 1, 4>(a, k1, perm, s); return;
+        case 3: launch_cfg3<T, TO, 256, 128, 4, 2>(a, k1, perm, s); return;
+        case 4: launch_cfg3<T, TO, 256, 256, 4, 2>(a, k1, perm, s); return;
+        case 5: launch_cfg3<T, TO, 256, 64, 4, 1>(a, k1, perm, s); return;
+        default: break;
+    }
+    // A-stationary variants (single output-channel tile, short K)
+    const int nk = a.kp / (sizeof(T) == 2 ? 64 : 32);
+    if (g_force_cfg == 6 || (g_force_cfg == 0 && g_ast)) {
+        if (a.cout > 128 && a.cout <= 256 && nk <= 1 && a.P > 64) {
+            launch_ns<T, TO, 256, 64, 4, 1, 2, 1>(a, k1, perm, s);
+            return;
+        }
+        if (a.cout <= 64 && nk <= 4 && a.P > 64) {
+            launch_ns<T, TO, 64, 128, 1, 4, 2, 4>(a, k1, perm, s);
+            return;
+        }
+        if (a.cout <= 64 && nk <= 9 && a.P > 64 && g_force_cfg == 6) {
+            launch_ns<T, TO, 64, 128, 1, 4, 2, 9>(a, k1, perm, s);
+            return;
+        }
+    }
     if (a.P <= 32)
         launch_cfg3<T, TO, 256, 32, 4, 1>(a, k1, perm, s);
     else if (a.P <= 64)
@@ -503,6 +547,14 @@ void launch_gemm2(const ConvArgs& a, bool k1, hipStream_t s) {
         launch_cfg3<T, TO, 256, 128, 4, 2>(a, k1, perm, s);   // 8 waves, 64x64 per wave
     else
         launch_cfg3<T, TO, 128, 128, 2, 2>(a, k1, perm, s);
+}
+
+void set_gemm_tuning(int key, int value) {
+    num_cus();
+    if (key == RR_TUNE_GEMM_CONFIG) g_force_cfg = value;
+    else if (key == RR_TUNE_GEMM_STAGES) g_stages = value == 3 ? 3 : 2;
+    else if (key == RR_TUNE_GEMM_WIDE) g_wide = value != 0;
+    else if (key == RR_TUNE_GEMM_ASTAT) g_ast = value != 0;
 }
 
 template void launch_gemm2<bf16_t, bf16_t>(const ConvArgs&, bool, hipStream_t);

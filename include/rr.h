@@ -151,6 +151,18 @@ int rr_knn_topk(const void* db, const float* db_f32, long long n_db,
 int rr_topk_merge(const double* in_scores, const long long* in_idx, int r, int nq, int k_in,
                   int k, double* out_scores, long long* out_idx, void* stream);
 
+/* ------------------------------------------------------------ tuning */
+/* Engine tuning knobs (process-wide; for benchmarking / autotuning tools):
+ *   RR_TUNE_GEMM_CONFIG  0 = automatic tile choice, 1 = 128x128, 2 = 64x256,
+ *                        3 = 256x128 (8 waves), 4 = 256x256 (8 waves), 5 = 256x64
+ *                        6 = A-stationary (weights resident in LDS) where eligible
+ *   RR_TUNE_GEMM_STAGES  2 or 3 LDS stages (3: one resident block per CU)
+ *   RR_TUNE_GEMM_WIDE    0/1 allow the 8-wave tiles in the automatic choice
+ *   RR_TUNE_GEMM_ASTAT   0/1 allow the A-stationary tiles in the automatic choice */
+enum rr_tune_key { RR_TUNE_GEMM_CONFIG = 0, RR_TUNE_GEMM_STAGES = 1, RR_TUNE_GEMM_WIDE = 2,
+                   RR_TUNE_GEMM_ASTAT = 3 };
+int rr_set_tuning(int key, int value);
+
 /* ----------------------------------------------------------- data helpers */
 /* Counter-based N(0,1) rows, each L2-normalised: row i of the global matrix
  * depends only on (seed, i0 + i), so shards generate identical rows. */

@@ -36,6 +36,31 @@ CONV_CASES = [
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
 @pytest.mark.parametrize("perm", [False, True])
 def test_conv_fused(cuda, case, prec, perm):
+    _check_conv(cuda, case, prec, perm)
+
+
+TILE_CASES = CONV_CASES + [
+    (2, 256, 20, 24, 256, 1, 1, 0, True, True),    # one channel tile, one K-step (A-stationary 256x64)
+    (2, 64, 21, 23, 64, 3, 1, 1, False, True),     # 64 channels, 9 K-steps
+    (2, 128, 18, 20, 64, 1, 1, 0, False, True),    # 64 channels, 2 K-steps
+]
+
+
+@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("case", TILE_CASES)
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_conv_tile_configs(cuda, cfg, case, prec):
+    """Every forced tile configuration of the GEMM engine (rr_set_tuning) is
+    exact on every conv shape — the automatic choice may pick any of them."""
+    from cirtorch import _engine as E
+    E.check(E.lib().rr_set_tuning(0, cfg), "rr_set_tuning")
+    try:
+        _check_conv(cuda, case, prec, True)
+    finally:
+        E.lib().rr_set_tuning(0, 0)
+
+
+def _check_conv(cuda, case, prec, perm):
     n, cin, h, w, cout, k, s, p, use_res, leaky = case
     g = torch.Generator().manual_seed(hash(case) & 0xFFFF)
     x = torch.randn(n, cin, h, w, generator=g)

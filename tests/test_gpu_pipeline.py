@@ -1,0 +1,93 @@
+"""End-to-end pipelines on the GPU engine:
+* the upstream ``extract_vectors`` front end on real image files (PIL decode,
+  longest side -> image_size, ToTensor + Normalize semantics, ms/msp rule);
+* config 4's flow: extract DB + query descriptors, GPU full ranks, mAP with the
+  reference protocol — ranks identical to ``np.argsort`` on the same vectors,
+  mAP equal to the oracle's on the oracle's descriptors within 1e-3."""
+
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import cosines
+
+pytestmark = pytest.mark.gpu
+
+MEAN, STD = [0.485, 0.456, 0.406], [0.229, 0.224, 0.225]
+
+
+def _product_and_oracle(arch, cuda):
+    from cirtorch.models.GF_net import make_net
+    from oracle import backbone as obb, weights
+    bs = weights.backbone_state(arch)
+    hs = weights.head_state(weights.OUTPUT_DIM[arch])
+    net = make_net(arch, precision="fp32", mean=MEAN, std=STD)
+    net.body.load_state_dict({k: torch.from_numpy(v) for k, v in bs.items()}, strict=False)
+    net.ret_head.load_state_dict({k: torch.from_numpy(v) for k, v in hs.items()})
+    return net.to(cuda).eval(), obb.OracleNet(arch, bs, hs)
+
+
+def test_extract_vectors_from_image_files(cuda, tmp_path):
+    from PIL import Image
+    from cirtorch.models.GF_net import extract_vectors, _load_pil, _to_tensor
+    from oracle import data, backbone as obb
+    net, onet = _product_and_oracle("resnet18", cuda)
+    paths = []
+    imgs = data.structured_images(3, 150, 200, seed=41)
+    for i, im in enumerate(imgs):
+        arr = (np.clip(im.transpose(1, 2, 0), 0, 1) * 255).astype(np.uint8)
+        p = os.path.join(str(tmp_path), "im%d.png" % i)
+        Image.fromarray(arr).save(p)
+        paths.append(p)
+    bbxs = [None, (10, 20, 120, 140), None]
+    # msp = p only applies to un-whitened GeM nets upstream (scripts/test.py:136-137); whitened -> msp = 1
+    for ms, msp in (([1], 1), ([1, 0.5], 1.0)):
+        vecs = extract_vectors(net, paths, 96, ms=ms, msp=msp, bbxs=[b if b else (0, 0, 200, 150) for b in bbxs])
+        assert vecs.shape == (512, 3)
+        # oracle on the same decoded tensors
+        for i, p in enumerate(paths):
+            x = _to_tensor(_load_pil(p, 96, bbxs[i] if bbxs[i] else (0, 0, 200, 150)))
+            xn = obb.normalize_images(x)
+            if ms == [1]:
+                ref = onet.forward([xn], normalize=False)[:, 0]
+            else:
+                acc = 0
+                for s in ms:
+                    xs = xn if s == 1 else torch.nn.functional.interpolate(
+                        xn[None], scale_factor=s, mode="bilinear", align_corners=False)[0]
+                    acc = acc + onet.forward([xs], normalize=False)[:, 0].double() ** msp
+                ref = (acc / len(ms)) ** (1.0 / msp)
+                ref = ref / ref.norm()
+            assert cosines(vecs[:, i:i + 1].numpy(), ref[:, None].numpy())[0] > 1 - 1e-4
+
+
+def test_config4_rank_and_map(cuda):
+    """roxford-shaped flow on a small synthetic set: descriptors from the
+    engine, ranks on the GPU, mAP with the revisited protocol."""
+    from cirtorch.search import rank
+    from cirtorch.utils.evaluation.ParisOxfordEval import compute_map_and_print
+    from oracle import data, ops, backbone as obb
+    net, onet = _product_and_oracle("resnet18", cuda)
+    ndb, nq = 60, 6
+    db_imgs = data.structured_images(ndb, 64, 80, seed=51)
+    q_imgs = db_imgs[:nq] * 0.9 + 0.05          # queries = perturbed copies of the first DB images
+    to_dev = [torch.from_numpy(im).to(cuda) for im in db_imgs]
+    vecs = net.extract(to_dev).cpu()              # D x ndb
+    qvecs = net.extract([torch.from_numpy(im).to(cuda) for im in q_imgs]).cpu()
+    ref_vecs = onet.forward([torch.from_numpy(im) for im in db_imgs]).numpy()
+    ref_q = onet.forward([torch.from_numpy(im) for im in q_imgs]).numpy()
+    assert cosines(vecs.numpy(), ref_vecs).min() > 1 - 1e-4
+    # GPU full ranks == np.argsort on the same vectors (exact fp64 order; stable ties)
+    ranks = rank(vecs, qvecs).cpu().numpy()
+    ref_ranks = np.argsort(-np.dot(vecs.double().numpy().T, qvecs.double().numpy()), axis=0, kind="stable")
+    np.testing.assert_array_equal(ranks, ref_ranks)
+    # mAP vs the oracle pipeline (reference descriptors + numpy rank)
+    r = data.rng(52)
+    gnd = [{"easy": np.array([i]), "hard": r.choice(np.arange(nq, ndb), 2, replace=False),
+            "junk": np.array([], dtype=np.int64)} for i in range(nq)]
+    got = compute_map_and_print("roxford5k", ranks, gnd, lambda *a: None)
+    _, oranks = ops.rank_reference(ref_vecs.T.copy(), ref_q.T.copy())
+    ref = ops.compute_map_revisited(oranks, gnd)
+    assert abs(got["mAP"] - 100 * (ref["mapM"] + ref["mapH"]) / 2) < 1e-3 * 100
