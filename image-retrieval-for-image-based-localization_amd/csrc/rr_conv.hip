@@ -297,6 +297,8 @@ static void launch(const ConvArgs& a, bool k1, hipStream_t s) {
 }
 
 template <typename T, typename TO> void launch_gemm2(const ConvArgs& a, bool k1, hipStream_t s);
+bool launch_stream1x1(const ConvArgs& a, hipStream_t s);  // rr_stream.hip
+extern int g_stream_mode;
 
 // out[R][k] = w[chan(R)][ci][kh][kw] with k = (kh*KW + kw)*cin_pad + ci, zeros elsewhere.
 template <typename T>
@@ -330,6 +332,9 @@ static bool use_v2(const ConvArgs& a, int dtype) {
 
 template <typename T, typename TO>
 static void dispatch(const ConvArgs& a, bool k1, int dtype, hipStream_t s) {
+    if constexpr (sizeof(T) == 2 && sizeof(TO) == 2) {
+        if (k1 && launch_stream1x1(a, s)) return;
+    }
     if (use_v2(a, dtype)) launch_gemm2<T, TO>(a, k1, s);
     else launch<T, TO>(a, k1, s);
 }
@@ -401,7 +406,8 @@ namespace rr {
 void set_gemm_tuning(int key, int value);
 }
 extern "C" int rr_set_tuning(int key, int value) {
-    if (key < 0 || key > 3) return fail(RR_EINVAL, "rr_set_tuning: unknown key");
-    rr::set_gemm_tuning(key, value);
+    if (key < 0 || key > 5) return fail(RR_EINVAL, "rr_set_tuning: unknown key");
+    if (key == RR_TUNE_STREAM_1X1) rr::g_stream_mode = value;
+    else rr::set_gemm_tuning(key, value);
     return RR_OK;
 }

@@ -103,7 +103,7 @@ template <> struct St4<bf16_t> {
 // into LDS once per block and only the activation tile streams through the
 // ring — the per-CU LDS-DMA volume drops to the B operand alone.
 template <typename T, typename TO, int TC, int TP, int WC, int WP, bool K1, bool PERM, int NS, int AK>
-__global__ void __launch_bounds__(64 * WC * WP, ((NS == 2 && AK * TC <= 256) || WC * WP == 8 ? 2 : 1)) k_igemm(ConvArgs a, int tiles_p, int ntiles) {
+__global__ void __launch_bounds__(64 * WC * WP, ((NS == 2 && AK * TC <= 256) || WC * WP == 8 ? 2 : 1)) k_igemm(ConvArgs a, int tiles_p, int ntiles, int xmap) {
     constexpr int VEC = Vec2<T>::N;
     constexpr int BK = 8 * VEC;               // elements per K-step (128 B per row)
     constexpr int ESZ = sizeof(T);
@@ -132,6 +132,21 @@ __global__ void __launch_bounds__(64 * WC * WP, ((NS == 2 && AK * TC <= 256) || 
     const int nk = a.kp / BK;
     const int my_tiles = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
     const int total = my_tiles * nk;
+    // XCD-aware tile order: workgroups are placed round-robin over the 8 XCDs
+    // (blockIdx % 8), so logical tile t runs on XCD t % 8.  Re-map it so each
+    // XCD sweeps a contiguous range of pixel tiles: the im2col taps a tile
+    // shares with its neighbours (rows above / below) are then L2 hits on the
+    // same XCD instead of Infinity-Cache reads.  A bijection on [0, ntiles).
+    // Within an XCD's range the order is pixel-tile-major, so the channel tiles
+    // of one pixel tile run side by side and share its activations in L2.
+    const int n8 = xmap ? ntiles & ~7 : 0, per8 = n8 >> 3;
+    const int tiles_c = ntiles / tiles_p;
+    auto tile_at = [&](int lt) {  // -> channel-major tile index (c0 = t / tiles_p)
+        const int t = (int)blockIdx.x + lt * (int)gridDim.x;
+        if (!xmap) return t;
+        const int q = t < n8 ? (t & 7) * per8 + (t >> 3) : t;
+        return (q % tiles_c) * tiles_p + q / tiles_c;
+    };
 
     // ---- issue-side state (tile whose K-steps are being fetched)
     i32x4_t rsA;
@@ -170,7 +185,7 @@ __global__ void __launch_bounds__(64 * WC * WP, ((NS == 2 && AK * TC <= 256) || 
     };
 
     auto issue = [&](int stage) {  // fetch step (is_tile, is_k) into `stage`, then advance
-        if (is_k == 0) setup_tile((int)blockIdx.x + is_tile * (int)gridDim.x);
+        if (is_k == 0) setup_tile(tile_at(is_tile));
         const int k0 = is_k * BK;
         const unsigned As = lds0 + stage * STAGE;
         const unsigned Bs = AK ? lds0 + ABYTES + stage * STAGE : As + TC * 128;
@@ -308,10 +323,10 @@ __global__ void __launch_bounds__(64 * WC * WP, ((NS == 2 && AK * TC <= 256) || 
                     }
                     if constexpr (sizeof(TO) == 2) {
                         uint4 q;
-                        q.x = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
-                        q.y = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
-                        q.z = (unsigned)f2bf(v[4]) | ((unsigned)f2bf(v[5]) << 16);
-                        q.w = (unsigned)f2bf(v[6]) | ((unsigned)f2bf(v[7]) << 16);
+                        q.x = pack_bf16x2(v[0], v[1]);
+                        q.y = pack_bf16x2(v[2], v[3]);
+                        q.z = pack_bf16x2(v[4], v[5]);
+                        q.w = pack_bf16x2(v[6], v[7]);
                         *reinterpret_cast<uint4*>(Y + o) = q;
                     } else {
                         St4<TO>::st(Y + o, v);
@@ -377,7 +392,7 @@ __global__ void __launch_bounds__(64 * WC * WP, ((NS == 2 && AK * TC <= 256) || 
         if constexpr (XPREF) {
             if (is_k == 1 % nk || nk == 1) {
                 const int lt = is_k == 0 ? is_tile - 1 : is_tile;  // local index of the tile just opened
-                const int t = (int)blockIdx.x + lt * (int)gridDim.x;
+                const int t = tile_at(lt);
                 if (lt & 1) prefetch_res(B1{}, t);
                 else prefetch_res(B0{}, t);
             }
@@ -399,7 +414,7 @@ __global__ void __launch_bounds__(64 * WC * WP, ((NS == 2 && AK * TC <= 256) || 
         else if (ahead == 1) wait_vm_barrier<AK ? NIB : NLD>();  // AK: a step issues B only (A's one-time load is older)
         else wait_vm_barrier<0>();
         if constexpr (!XPREF) {
-            if (ck == nk - 1) prefetch_res(B0{}, (int)blockIdx.x + ctile * (int)gridDim.x);
+            if (ck == nk - 1) prefetch_res(B0{}, tile_at(ctile));
         }
         const char* As = AK ? smem + ck * TC * 128 : smem + cur * STAGE;
         const char* Bs = AK ? smem + ABYTES + cur * STAGE : As + TC * 128;
@@ -434,7 +449,7 @@ __global__ void __launch_bounds__(64 * WC * WP, ((NS == 2 && AK * TC <= 256) || 
         }
         lds_barrier();  // every wave finished reading stage `cur` before it is refilled
         if (++ck == nk) {
-            const int t = (int)blockIdx.x + ctile * (int)gridDim.x;
+            const int t = tile_at(ctile);
             if constexpr (XPREF) {
                 if (ctile & 1) epilogue(B1{}, t);
                 else epilogue(B0{}, t);
@@ -455,6 +470,7 @@ static int g_num_cus = 0;
 static int g_stages = 0;
 static bool g_wide = true;
 static bool g_ast = false;
+static bool g_xmap = false;
 
 static int num_cus() {
     if (g_num_cus == 0) {
@@ -482,7 +498,7 @@ static void launch_ns(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
     const int cap = PER_CU * num_cus();
     const int grid = ntiles < cap ? ntiles : cap;
 #define RR_L3(K1V, PV) \
-    hipLaunchKernelGGL((k_igemm<T, TO, TC, TP, WC, WP, K1V, PV, NS, AK>), dim3(grid), dim3(64 * WC * WP), 0, s, a, tiles_p, ntiles)
+    hipLaunchKernelGGL((k_igemm<T, TO, TC, TP, WC, WP, K1V, PV, NS, AK>), dim3(grid), dim3(64 * WC * WP), 0, s, a, tiles_p, ntiles, g_xmap ? 1 : 0)
     if constexpr (sizeof(T) == sizeof(TO) && (TC / WC / 16) % 2 == 0) {
         if (perm) {
             if (k1) RR_L3(true, true); else RR_L3(false, true);
@@ -510,7 +526,8 @@ int g_force_cfg = 0;  // rr_set_tuning(RR_TUNE_GEMM_CONFIG, ...)
 template <typename T, typename TO>
 void launch_gemm2(const ConvArgs& a, bool k1, hipStream_t s) {
     const bool perm = (a.flags & RR_CONV_PERM32) != 0;
-    const int cus = num_cus();
+    const bool resid = (a.flags & RR_CONV_RESIDUAL) != 0;
+    num_cus();
     switch (g_force_cfg) {
         case 1: launch_cfg3<T, TO, 128, 128, 2, 2>(a, k1, perm, s); return;
         case 2: launch_cfg3<T, TO, 64, 256, 1, 4>(a, k1, perm, s); return;
@@ -535,18 +552,25 @@ void launch_gemm2(const ConvArgs& a, bool k1, hipStream_t s) {
             return;
         }
     }
+    // Automatic choice (per-shape sweep, tools/tune_layers.py, R50 @ 32 x 768x1024):
+    //  * small P: one row of pixel tiles, channel-wide
+    //  * c_out = 64: 64x256; c_out = 128: 128x128
+    //  * residual 1x1 into 256 channels with one K-step: A-stationary 256x64
+    //  * residual, K < 512: 256x128 (8 waves); everything else >= 256 channels: 256x256 (8 waves)
     if (a.P <= 32)
         launch_cfg3<T, TO, 256, 32, 4, 1>(a, k1, perm, s);
     else if (a.P <= 64)
         launch_cfg3<T, TO, 256, 64, 4, 1>(a, k1, perm, s);
     else if (a.cout <= 64)
         launch_cfg3<T, TO, 64, 256, 1, 4>(a, k1, perm, s);
-    else if (g_wide && a.kp >= 512 && a.cout >= 256 && (long long)((a.P + 255) / 256) * ((a.cout + 255) / 256) >= cus)
-        launch_cfg3<T, TO, 256, 256, 4, 2>(a, k1, perm, s);   // 8 waves, 64x128 per wave
-    else if (g_wide && a.kp >= 512 && a.cout >= 256 && (long long)((a.P + 127) / 128) * ((a.cout + 255) / 256) >= cus)
-        launch_cfg3<T, TO, 256, 128, 4, 2>(a, k1, perm, s);   // 8 waves, 64x64 per wave
-    else
+    else if (a.cout <= 128 || !g_wide)
         launch_cfg3<T, TO, 128, 128, 2, 2>(a, k1, perm, s);
+    else if (resid && a.cout <= 256 && nk <= 1)
+        launch_ns<T, TO, 256, 64, 4, 1, 2, 1>(a, k1, perm, s);
+    else if (resid && a.kp < 512)
+        launch_cfg3<T, TO, 256, 128, 4, 2>(a, k1, perm, s);
+    else
+        launch_cfg3<T, TO, 256, 256, 4, 2>(a, k1, perm, s);
 }
 
 void set_gemm_tuning(int key, int value) {
@@ -555,6 +579,7 @@ void set_gemm_tuning(int key, int value) {
     else if (key == RR_TUNE_GEMM_STAGES) g_stages = value == 3 ? 3 : 2;
     else if (key == RR_TUNE_GEMM_WIDE) g_wide = value != 0;
     else if (key == RR_TUNE_GEMM_ASTAT) g_ast = value != 0;
+    else if (key == RR_TUNE_GEMM_XCD_MAP) g_xmap = value != 0;
 }
 
 template void launch_gemm2<bf16_t, bf16_t>(const ConvArgs&, bool, hipStream_t);

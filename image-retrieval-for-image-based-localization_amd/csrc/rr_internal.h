@@ -27,17 +27,26 @@ typedef uint16_t bf16_t;
 
 __device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 
-// round-to-nearest-even float -> bf16 (NaN kept NaN by the explicit branch).
+// round-to-nearest-even float -> bf16, NaN kept NaN.  On the device this is
+// the gfx950 v_cvt_pk_bf16_f32 instruction (branch-free; the bit-twiddling
+// form compiles to an exec-masked branch per element); the host form is the
+// same rounding in integer arithmetic.
+typedef __attribute__((ext_vector_type(2))) float f32x2_cvt_t;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_cvt_t;
 __device__ __host__ __forceinline__ bf16_t f2bf(float f) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    uint32_t u = __float_as_uint(f);
+    return __builtin_bit_cast(bf16_t, (__bf16)f);
 #else
     uint32_t u;
     __builtin_memcpy(&u, &f, 4);
-#endif
     if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return (bf16_t)((u >> 16) | 0x40);
     u += 0x7fffu + ((u >> 16) & 1u);
     return (bf16_t)(u >> 16);
+#endif
+}
+// two floats -> packed bf16x2 (lo in bits 0..15), one v_cvt_pk_bf16_f32.
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_cvt_t){lo, hi}, bf16x2_cvt_t));
 }
 
 template <typename T> struct DT;

@@ -1,0 +1,261 @@
+// librr.so — streaming 1x1 conv for the HBM-bound bottleneck layers (bf16).
+//
+// The 1x1 convolutions of a bottleneck (conv1 / conv3 / projection) have
+// K = 64..512: a few MFMAs per byte, so they are bound by HBM, not by the
+// matrix cores (ResNet-50 @ 32 x 1024x768: ~60 % of conv time).  The tiled
+// LDS-DMA engine (rr_gemm.hip) loses there because one wave's vmcnt counts
+// its epilogue stores together with its next tile's DMA: every tile waits for
+// its own stores to drain, which serialises the memory pipeline.
+//
+// This kernel is weight-stationary and barrier-free after the prologue:
+//   * a block holds one slice of TC output channels x all K input channels of
+//     the (PERM32-packed) weights in LDS, loaded once;
+//   * every wave then streams its own 16*FN-pixel strips: activations go
+//     HBM -> VGPR directly in the MFMA B-operand layout (no LDS round trip),
+//     D strips deep (rotating register sets, compiler-tracked vmcnt — all
+//     VMEM traffic is visible to the compiler, so a wait for strip j's
+//     operands never waits for the stores of strips < j);
+//   * the residual rows are prefetched the same way, D strips ahead;
+//   * fused epilogue: BN scale/shift (from LDS), + residual, leaky ReLU,
+//     bf16 pack, one 16-B store per (fragment pair, pixel).
+// HBM traffic = x once (per channel slice) + residual once + y once.
+#include "rr_internal.h"
+
+namespace rr {
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 sbf16x8_t;
+typedef __attribute__((ext_vector_type(4))) float sf32x4_t;
+
+// LDS image of the weight slice: row r (packed output channel), 16-B chunk c
+// lives at r*K*2 + ((c ^ f(r)) * 16); f makes every ds_read_b128 lane group of
+// an A-fragment read hit 16 distinct 4-bank groups (checked for K = 64..1024).
+template <int K>
+__device__ __forceinline__ int wswz(int row, int chunk) {
+    const int f = K == 64 ? ((row >> 1) & 7) : (row & 15);
+    return row * (K * 2) + ((chunk ^ f) << 4);
+}
+
+template <int TC, int K, int FN, int D, int NW, bool RES>
+__global__ void __launch_bounds__(64 * NW) k_stream1x1(ConvArgs a, int nslices) {
+    constexpr int NI = TC / 16;   // accumulator fragments (channels) per wave
+    constexpr int NK = K / 32;    // MFMA K-steps
+    constexpr int NR = TC / 32;   // 16-B epilogue vectors per pixel
+    constexpr int SP = 16 * FN;   // pixels per strip
+    constexpr bool AREG = NI * NK * 4 <= 32;  // small slices keep A in VGPRs
+    __shared__ __attribute__((aligned(16))) char sA[TC * K * 2];
+    __shared__ __attribute__((aligned(16))) float sS[TC], sH[TC];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int slice = (int)blockIdx.x % nslices;
+    const int bi = (int)blockIdx.x / nslices;
+    const int G = (int)gridDim.x / nslices;
+    const int c0 = slice * TC;
+
+    // ---- prologue: weight slice + affine into LDS (once per block)
+    {
+        const char* wsrc = (const char*)a.w + (long long)c0 * K * 2;
+        constexpr int CH = TC * K / 8;  // 16-B chunks
+        for (int i = tid; i < CH; i += 64 * NW) {
+            const int r = i / (K / 8), c = i - r * (K / 8);
+            *reinterpret_cast<uint4*>(sA + wswz<K>(r, c)) = *reinterpret_cast<const uint4*>(wsrc + (long long)i * 16);
+        }
+        const bool affine = a.flags & RR_CONV_AFFINE;
+        for (int i = tid; i < TC; i += 64 * NW) {
+            sS[i] = affine ? a.scale[c0 + i] : 1.f;
+            sH[i] = affine ? a.shift[c0 + i] : 0.f;
+        }
+    }
+    __syncthreads();
+
+    const int r16 = lane & 15, kq = lane >> 4;
+    const long long P = a.P;
+    const int nstrips = (int)((P + SP - 1) / SP);
+    const int gw = bi * NW + wave, GW = G * NW;
+    const int nmine = gw < nstrips ? (nstrips - gw + GW - 1) / GW : 0;
+    if (nmine == 0) return;
+    const int niter = (nmine + D - 1) / D * D;
+    const int hw = a.ho * a.wo;
+    const bf16_t* __restrict__ X = (const bf16_t*)a.x;
+    const bf16_t* __restrict__ R = (const bf16_t*)a.res;
+    bf16_t* __restrict__ Y = (bf16_t*)a.y;
+    const bool leaky = a.act == RR_ACT_LEAKY;
+    const float slope = a.slope;
+
+    // strip i of this wave (clamped past the end: loads stay in range, stores are skipped)
+    auto strip_of = [&](int i) { return gw + (i < nmine ? i : nmine - 1) * GW; };
+    auto pix = [&](int s, int j) {  // this lane's pixel in fragment j of strip s (clamped)
+        long long p = (long long)s * SP + j * 16 + r16;
+        return p < P ? p : P - 1;
+    };
+    auto x_off = [&](long long p) {  // element offset of pixel p's input row
+        const long long img = p / hw;
+        const int rem = (int)(p - img * hw);
+        const int oh = rem / a.wo, ow = rem - oh * a.wo;
+        return ((img * a.h + (long long)oh * a.stride) * a.w_ + (long long)ow * a.stride) * K;
+    };
+
+    uint4 bq[D][FN][NK];
+    uint4 rq[RES ? D : 1][RES ? FN : 1][RES ? NR : 1];
+    auto load_b = [&](uint4 (&dst)[FN][NK], int s) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+            const bf16_t* src = X + x_off(pix(s, j)) + 8 * kq;
+#pragma unroll
+            for (int kk = 0; kk < NK; ++kk) dst[j][kk] = *reinterpret_cast<const uint4*>(src + kk * 32);
+        }
+    };
+    auto load_r = [&](uint4 (&dst)[RES ? FN : 1][RES ? NR : 1], int s) {
+        if constexpr (RES) {
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+                const bf16_t* src = R + pix(s, j) * a.ldy + c0 + 8 * kq;
+#pragma unroll
+                for (int i2 = 0; i2 < NR; ++i2) dst[j][i2] = *reinterpret_cast<const uint4*>(src + 32 * i2);
+            }
+        }
+    };
+
+    uint4 areg[AREG ? NI : 1][AREG ? NK : 1];
+    if constexpr (AREG) {
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int kk = 0; kk < NK; ++kk)
+                areg[i][kk] = *reinterpret_cast<const uint4*>(sA + wswz<K>(i * 16 + r16, kk * 4 + kq));
+    }
+
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        load_b(bq[d], strip_of(d));
+        load_r(rq[RES ? d : 0], strip_of(d));
+    }
+
+    for (int it = 0; it < niter; it += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const int i = it + d;
+            const int s = strip_of(i);
+            const bool live = i < nmine;
+            // one 32-channel group at a time: 2 x FN accumulators, epilogue right away
+#pragma unroll
+            for (int i2 = 0; i2 < NR; ++i2) {
+                // opaque LDS base: keeps the compiler from hoisting every A fragment of
+                // the (loop-invariant) weight slice into VGPRs, which would spill
+                int abase = 0;
+                asm volatile("" : "+v"(abase));
+                sf32x4_t acc[2][FN];
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+#pragma unroll
+                    for (int j = 0; j < FN; ++j) acc[h][j] = (sf32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int kk = 0; kk < NK; ++kk)
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int ii = 2 * i2 + h;
+                        const uint4 av = AREG ? areg[AREG ? ii : 0][AREG ? kk : 0]
+                                              : *reinterpret_cast<const uint4*>(sA + abase + wswz<K>(ii * 16 + r16, kk * 4 + kq));
+#pragma unroll
+                        for (int j = 0; j < FN; ++j)
+                            acc[h][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(sbf16x8_t, av),
+                                                                                __builtin_bit_cast(sbf16x8_t, bq[d][j][kk]),
+                                                                                acc[h][j], 0, 0, 0);
+                    }
+                if (live) {
+                    const int cl = 32 * i2 + 8 * kq;  // 8 consecutive channels of this lane
+                    const float4 sc0 = *reinterpret_cast<const float4*>(sS + cl);
+                    const float4 sc1 = *reinterpret_cast<const float4*>(sS + cl + 4);
+                    const float4 sh0 = *reinterpret_cast<const float4*>(sH + cl);
+                    const float4 sh1 = *reinterpret_cast<const float4*>(sH + cl + 4);
+                    const float sc[8] = {sc0.x, sc0.y, sc0.z, sc0.w, sc1.x, sc1.y, sc1.z, sc1.w};
+                    const float sh[8] = {sh0.x, sh0.y, sh0.z, sh0.w, sh1.x, sh1.y, sh1.z, sh1.w};
+#pragma unroll
+                    for (int j = 0; j < FN; ++j) {
+                        const long long p = (long long)s * SP + j * 16 + r16;
+                        float v[8];
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            v[r] = acc[0][j][r] * sc[r] + sh[r];
+                            v[4 + r] = acc[1][j][r] * sc[4 + r] + sh[4 + r];
+                        }
+                        if constexpr (RES) {
+                            const uint4 q = rq[d][j][i2];
+                            const unsigned w4[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                v[2 * r] += __uint_as_float(w4[r] << 16);
+                                v[2 * r + 1] += __uint_as_float(w4[r] & 0xffff0000u);
+                            }
+                        }
+                        if (leaky) {
+#pragma unroll
+                            for (int r = 0; r < 8; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * slope;
+                        }
+                        uint4 o;
+                        o.x = pack_bf16x2(v[0], v[1]);
+                        o.y = pack_bf16x2(v[2], v[3]);
+                        o.z = pack_bf16x2(v[4], v[5]);
+                        o.w = pack_bf16x2(v[6], v[7]);
+                        if (p < P) *reinterpret_cast<uint4*>(Y + p * a.ldy + c0 + cl) = o;
+                    }
+                }
+            }
+            load_b(bq[d], strip_of(i + D));  // refill: strip i + D
+            load_r(rq[RES ? d : 0], strip_of(i + D));
+        }
+    }
+}
+
+int g_stream_cus = 0;
+
+template <int TC, int K, int FN, int D, int NW>
+void launch_s(const ConvArgs& a, hipStream_t s) {
+    if (g_stream_cus == 0) {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 256;
+        g_stream_cus = cus;
+    }
+    constexpr int LDS = TC * K * 2 + TC * 8;
+    constexpr int PER_CU = (160 * 1024 / LDS) >= 2 && NW <= 8 ? (NW <= 4 ? 4 : 2) : 1;
+    const int nslices = a.cout / TC;
+    const long long nstrips = ((long long)a.P + 16 * FN - 1) / (16 * FN);
+    long long per_slice = (long long)PER_CU * g_stream_cus / nslices;
+    if (per_slice < 1) per_slice = 1;
+    const long long need = (nstrips + NW - 1) / NW;
+    if (per_slice > need) per_slice = need;
+    const int grid = (int)(per_slice * nslices);
+    if (a.flags & RR_CONV_RESIDUAL)
+        hipLaunchKernelGGL((k_stream1x1<TC, K, FN, D, NW, true>), dim3(grid), dim3(64 * NW), 0, s, a, nslices);
+    else
+        hipLaunchKernelGGL((k_stream1x1<TC, K, FN, D, NW, false>), dim3(grid), dim3(64 * NW), 0, s, a, nslices);
+}
+
+}  // namespace
+
+int g_stream_mode = 1;  // rr_set_tuning(RR_TUNE_STREAM_1X1): 0 off, 1 auto
+
+// bf16 1x1 (pad 0, any stride), PERM32 weights, bf16 out: returns false when the
+// shape is not one the streaming kernel is built for (caller uses the tiled engine).
+bool launch_stream1x1(const ConvArgs& a, hipStream_t s) {
+    if (g_stream_mode == 0) return false;
+    if (!(a.flags & RR_CONV_PERM32) || a.kh != 1 || a.kw != 1 || a.pad != 0 || a.kp != a.cin) return false;
+    if (a.P < 4096 || (long long)a.n * a.h * a.w_ * a.cin >= (1ll << 31)) return false;
+    const bool res = a.flags & RR_CONV_RESIDUAL;
+    const int K = a.cin, C = a.cout;
+    if (K == 64 && C == 64) { launch_s<64, 64, 2, 4, 8>(a, s); return true; }
+    if (K == 64 && C == 256) { launch_s<256, 64, 1, 2, 8>(a, s); return true; }
+    if (K == 256 && C == 64) { launch_s<64, 256, 1, 4, 8>(a, s); return true; }
+    if (K == 256 && C == 128) { launch_s<128, 256, 1, 3, 8>(a, s); return true; }
+    if (K == 128 && C == 512) { launch_s<256, 128, 1, 3, 8>(a, s); return true; }
+    if (K == 512 && C == 128) { launch_s<128, 512, 1, 2, 8>(a, s); return true; }
+    if (K == 256 && C == 1024 && res) { launch_s<256, 256, 1, 2, 8>(a, s); return true; }
+    if (K == 256 && C == 512 && !res) { launch_s<256, 256, 1, 2, 8>(a, s); return true; }
+    return false;
+}
+
+}  // namespace rr

@@ -158,9 +158,12 @@ int rr_topk_merge(const double* in_scores, const long long* in_idx, int r, int n
  *                        6 = A-stationary (weights resident in LDS) where eligible
  *   RR_TUNE_GEMM_STAGES  2 or 3 LDS stages (3: one resident block per CU)
  *   RR_TUNE_GEMM_WIDE    0/1 allow the 8-wave tiles in the automatic choice
- *   RR_TUNE_GEMM_ASTAT   0/1 allow the A-stationary tiles in the automatic choice */
+ *   RR_TUNE_GEMM_ASTAT   0/1 allow the A-stationary tiles in the automatic choice
+ *   RR_TUNE_GEMM_XCD_MAP 0/1 XCD-contiguous tile order (default 0)
+ *   RR_TUNE_STREAM_1X1   0/1 weight-stationary streaming kernel for the
+ *                        HBM-bound bf16 1x1 convs (default 1) */
 enum rr_tune_key { RR_TUNE_GEMM_CONFIG = 0, RR_TUNE_GEMM_STAGES = 1, RR_TUNE_GEMM_WIDE = 2,
-                   RR_TUNE_GEMM_ASTAT = 3 };
+                   RR_TUNE_GEMM_ASTAT = 3, RR_TUNE_GEMM_XCD_MAP = 4, RR_TUNE_STREAM_1X1 = 5 };
 int rr_set_tuning(int key, int value);
 
 /* ----------------------------------------------------------- data helpers */

@@ -60,6 +60,33 @@ def test_conv_tile_configs(cuda, cfg, case, prec):
         E.lib().rr_set_tuning(0, 0)
 
 
+STREAM_CASES = [
+    # HBM-bound bf16 1x1 shapes of the bottleneck blocks (rr_stream.hip), P >= 4096, ragged P
+    (2, 64, 47, 51, 64, 1, 1, 0, False, True),
+    (2, 64, 41, 59, 256, 1, 1, 0, True, True),
+    (2, 64, 41, 59, 256, 1, 1, 0, False, False),
+    (2, 256, 39, 53, 64, 1, 1, 0, False, True),
+    (2, 256, 39, 53, 128, 1, 1, 0, False, True),
+    (1, 128, 63, 71, 512, 1, 1, 0, True, True),
+    (1, 512, 63, 67, 128, 1, 1, 0, False, True),
+    (1, 256, 65, 67, 1024, 1, 1, 0, True, True),
+    (2, 256, 83, 101, 512, 1, 2, 0, False, False),   # strided projection
+]
+
+
+@pytest.mark.parametrize("case", STREAM_CASES)
+@pytest.mark.parametrize("mode", [1, 0])
+def test_conv_stream1x1(cuda, case, mode):
+    """The weight-stationary streaming 1x1 kernel (mode 1) and the tiled engine
+    (mode 0) on the same shapes."""
+    from cirtorch import _engine as E
+    E.check(E.lib().rr_set_tuning(5, mode), "rr_set_tuning")
+    try:
+        _check_conv(cuda, case, "bf16", True)
+    finally:
+        E.lib().rr_set_tuning(5, 1)
+
+
 def _check_conv(cuda, case, prec, perm):
     n, cin, h, w, cout, k, s, p, use_res, leaky = case
     g = torch.Generator().manual_seed(hash(case) & 0xFFFF)

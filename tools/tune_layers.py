@@ -61,25 +61,27 @@ def main():
         ts = sorted(a.elapsed_time(b) for a, b in ev)
         return ts[len(ts) // 2] * 1e3
 
-    variants = [(0, 2)] + [(c, 2) for c in CFG]
-    head = "%-14s %-26s" % ("layer", "P x Cout x K") + "".join("%10s" % ("auto" if c == 0 else CFG[c] + ("/3" if s == 3 else ""))
-                                                                 for c, s in variants)
+    # (label, {tuning key: value}); key 0 = tile config, 4 = XCD tile order
+    # (label, {tuning key: value}); key 0 = tile config, 5 = streaming 1x1 kernel
+    variants = [("auto", {0: 0, 5: 1}), ("auto/noS", {0: 0, 5: 0})] + \
+               [(CFG[c], {0: c, 5: 0}) for c in CFG]
+    head = "%-14s %-26s" % ("layer", "P x Cout x K") + "".join("%12s" % v[0] for v in variants)
     print(head)
     for name, inp, st, res in calls:
         n, h, w, c = inp.shape
         ho = (h + 2 * st.pad - st.kh) // st.stride + 1
         wo = (w + 2 * st.pad - st.kw) // st.stride + 1
         row = "%-14s %-26s" % (name, "%d x %d x %d" % (n * ho * wo, st.c_out, st.kh * st.kw * c))
-        for c_, s_ in variants:
-            E.lib().rr_set_tuning(0, c_)
-            E.lib().rr_set_tuning(1, s_)
+        for _, kv in variants:
+            for k_, v_ in kv.items():
+                E.lib().rr_set_tuning(k_, v_)
             try:
-                row += "%10.1f" % timeit(inp, st, res)
+                row += "%12.1f" % timeit(inp, st, res)
             except Exception:
-                row += "%10s" % "err"
+                row += "%12s" % "err"
         print(row, flush=True)
     E.lib().rr_set_tuning(0, 0)
-    E.lib().rr_set_tuning(1, 2)
+    E.lib().rr_set_tuning(5, 1)
 
 
 if __name__ == "__main__":
