@@ -19,6 +19,7 @@ Activations stay NHWC in HBM; the returned stage maps are NCHW-shaped
 ``channels_last`` views of those buffers (no copies).
 """
 
+import os
 import sys
 from collections import OrderedDict
 from functools import partial
@@ -174,6 +175,11 @@ class ResNet(nn.Module):
         if dev.type != "cuda":
             raise RuntimeError("the MI355X engine runs on the GPU: call .cuda() on the model first")
         plan = {"stem": self._step(self.mod1.conv1, self.mod1.bn1, cin_pad=self.stem_cin()), "mods": []}
+        # bf16: conv1 + bn1 + pool1 run as ONE fused kernel (rr_stem_conv_pool)
+        plan["stem_fused"] = None
+        if self.engine_dtype == torch.bfloat16 and tuple(self.mod1.conv1.weight.shape) == (64, 3, 7, 7) \
+                and hasattr(self.mod1, "pool1") and os.environ.get("RR_STEM_FUSED", "1") != "0":
+            plan["stem_fused"] = _ops.pack_stem_weights(self.mod1.conv1.weight)
         for mod_id in range(4):
             mod = getattr(self, "mod%d" % (mod_id + 2))
             blocks = []
@@ -202,9 +208,14 @@ class ResNet(nn.Module):
         ``normalize`` into the first kernel).  Returns OrderedDict mod1..mod5."""
         plan = self._plan or self._build_plan()
         mean, std = normalize if normalize is not None else (None, None)
-        t = _ops.image_to_nhwc(x, self.stem_cin(), self.engine_dtype, mean, std)
-        t = self._conv(t, plan["stem"])
-        t = _ops.maxpool2d(t, 3, 2, 1)
+        if plan["stem_fused"] is not None:
+            st = plan["stem"]
+            t = _ops.stem_conv_pool(x, plan["stem_fused"], st.scale, st.shift, leaky=st.leaky, slope=st.slope,
+                                    mean=mean, std=std)
+        else:
+            t = _ops.image_to_nhwc(x, self.stem_cin(), self.engine_dtype, mean, std)
+            t = self._conv(t, plan["stem"])
+            t = _ops.maxpool2d(t, 3, 2, 1)
         outs = OrderedDict()
         outs["mod1"] = t
         for mod_id, blocks in enumerate(plan["mods"]):

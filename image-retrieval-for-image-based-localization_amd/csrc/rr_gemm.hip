@@ -102,8 +102,11 @@ template <> struct St4<bf16_t> {
 // (c_out <= TC) and at most AK K-steps, so the whole weight slice is fetched
 // into LDS once per block and only the activation tile streams through the
 // ring — the per-CU LDS-DMA volume drops to the B operand alone.
-template <typename T, typename TO, int TC, int TP, int WC, int WP, bool K1, bool PERM, int NS, int AK>
+// KM (operand-B addressing): 1 = 1x1 / pad 0 (K1), 2 = im2col with c_in a multiple of the
+// 128-B K-step (every step inside one filter tap: wave-uniform tap, TAPU), 0 = generic im2col.
+template <typename T, typename TO, int TC, int TP, int WC, int WP, int KM, bool PERM, int NS, int AK>
 __global__ void __launch_bounds__(64 * WC * WP, ((NS == 2 && AK * TC <= 256) || WC * WP == 8 ? 2 : 1)) k_igemm(ConvArgs a, int tiles_p, int ntiles, int xmap) {
+    constexpr bool K1 = KM == 1, tapu = KM == 2;
     constexpr int VEC = Vec2<T>::N;
     constexpr int BK = 8 * VEC;               // elements per K-step (128 B per row)
     constexpr int ESZ = sizeof(T);
@@ -175,10 +178,10 @@ __global__ void __launch_bounds__(64 * WC * WP, ((NS == 2 && AK * TC <= 256) || 
                 b_hi[i] = oh * a.stride - a.pad;
                 b_wi[i] = ow * a.stride - a.pad;
                 long long base = (long long)img * H * W * Cin;
-                if (K1) base += ((long long)b_hi[i] * W + b_wi[i]) * Cin + lchunk * VEC;
-                b_base[i] = (unsigned)base;
+                if (K1 || tapu) base += ((long long)b_hi[i] * W + b_wi[i]) * Cin + lchunk * VEC;
+                b_base[i] = (unsigned)base;  // tapu: may wrap below 0; taps add back mod 2^32
             } else {
-                b_hi[i] = b_wi[i] = 0;
+                b_hi[i] = b_wi[i] = -(1 << 28);  // fails every tap's bounds check
                 b_base[i] = OOB;
             }
         }
@@ -205,11 +208,25 @@ __global__ void __launch_bounds__(64 * WC * WP, ((NS == 2 && AK * TC <= 256) || 
                 dma16(rsA, off, As + (wave + NW * i) * 1024);
             }
         }
+        int tap_dh = 0, tap_dw = 0, tap_add = 0;
+        if constexpr (tapu) {
+            const int tap = k0 >> a.lc, ci0 = k0 & (Cin - 1);
+            const int kh = tap / a.kw, kw = tap - kh * a.kw;
+            tap_dh = kh * a.dil;
+            tap_dw = kw * a.dil;
+            tap_add = (tap_dh * W + tap_dw) * Cin + ci0;
+        }
 #pragma unroll
         for (int i = 0; i < NIB; ++i) {
             unsigned off;
             if (K1) {
                 off = b_base[i] == OOB ? OOB : (b_base[i] + (unsigned)k0) * ESZ;
+            } else if constexpr (tapu) {
+                // c_in is a multiple of the 128-B K-step: the step lies inside one tap, so
+                // (kh, kw, ci0) are wave-uniform and a lane only re-checks its row's bounds
+                const int hi = b_hi[i] + tap_dh, wi = b_wi[i] + tap_dw;
+                const bool ok = (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
+                off = ok ? (b_base[i] + (unsigned)tap_add) * ESZ : OOB;
             } else {
                 const int k = k0 + lchunk * VEC;
                 const int tap = k >> a.lc;
@@ -497,15 +514,26 @@ static void launch_ns(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
     const int ntiles = tiles_p * tiles_c;
     const int cap = PER_CU * num_cus();
     const int grid = ntiles < cap ? ntiles : cap;
-#define RR_L3(K1V, PV) \
-    hipLaunchKernelGGL((k_igemm<T, TO, TC, TP, WC, WP, K1V, PV, NS, AK>), dim3(grid), dim3(64 * WC * WP), 0, s, a, tiles_p, ntiles, g_xmap ? 1 : 0)
+    const int km = k1 ? 1 : (a.cin * (int)sizeof(T)) % 128 == 0 ? 2 : 0;
+#define RR_L3(PV)                                                                                                    \
+    do {                                                                                                             \
+        if (km == 1)                                                                                                 \
+            hipLaunchKernelGGL((k_igemm<T, TO, TC, TP, WC, WP, 1, PV, NS, AK>), dim3(grid), dim3(64 * WC * WP), 0, s, \
+                               a, tiles_p, ntiles, g_xmap ? 1 : 0);                                                  \
+        else if (km == 2)                                                                                            \
+            hipLaunchKernelGGL((k_igemm<T, TO, TC, TP, WC, WP, 2, PV, NS, AK>), dim3(grid), dim3(64 * WC * WP), 0, s, \
+                               a, tiles_p, ntiles, g_xmap ? 1 : 0);                                                  \
+        else                                                                                                         \
+            hipLaunchKernelGGL((k_igemm<T, TO, TC, TP, WC, WP, 0, PV, NS, AK>), dim3(grid), dim3(64 * WC * WP), 0, s, \
+                               a, tiles_p, ntiles, g_xmap ? 1 : 0);                                                  \
+    } while (0)
     if constexpr (sizeof(T) == sizeof(TO) && (TC / WC / 16) % 2 == 0) {
         if (perm) {
-            if (k1) RR_L3(true, true); else RR_L3(false, true);
+            RR_L3(true);
             return;
         }
     }
-    if (k1) RR_L3(true, false); else RR_L3(false, false);
+    RR_L3(false);
 #undef RR_L3
 }
 
@@ -541,14 +569,6 @@ void launch_gemm2(const ConvArgs& a, bool k1, hipStream_t s) {
     if (g_force_cfg == 6 || (g_force_cfg == 0 && g_ast)) {
         if (a.cout > 128 && a.cout <= 256 && nk <= 1 && a.P > 64) {
             launch_ns<T, TO, 256, 64, 4, 1, 2, 1>(a, k1, perm, s);
-            return;
-        }
-        if (a.cout <= 64 && nk <= 4 && a.P > 64) {
-            launch_ns<T, TO, 64, 128, 1, 4, 2, 4>(a, k1, perm, s);
-            return;
-        }
-        if (a.cout <= 64 && nk <= 9 && a.P > 64 && g_force_cfg == 6) {
-            launch_ns<T, TO, 64, 128, 1, 4, 2, 9>(a, k1, perm, s);
             return;
         }
     }

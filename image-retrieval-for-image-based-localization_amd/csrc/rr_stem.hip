@@ -1,0 +1,284 @@
+// librr.so — fused ResNet stem (bf16): normalise + conv1 7x7/s2/p3 (3 -> 64)
+// + BN affine + activation + max-pool 3x3/s2/p1, one kernel.
+//
+// Replaces the reference's mod1 = Sequential(conv1, bn1, pool1)
+// (cirtorch/backbones/resnet.py:59-66) fed by utils/image.py:125 `normalize`.
+// The unfused path moves the 64-channel stride-2 map through HBM twice
+// (conv write + pool read: 4x the pooled bytes) and runs the 7x7 im2col
+// through the generic LDS-DMA engine at 8 padded channels per tap.
+//
+// Layout of the work, per block (one per CU, persistent over tiles):
+//   * pooled tile PH x PW  <-  stem tile (2PH+1) x (2PW+1)  <-  input patch
+//     (4PH+7) x (4PW+8) pixels of the fp32 NCHW image, normalised on the fly
+//     and staged in LDS as bf16 [row][col][4 ch] (8 B / pixel, channel 3 = 0);
+//     the next tile's patch is fetched into VGPRs while this tile computes;
+//   * K = 7 kh x 8 kw x 4 ch = 224 (kw = 7 and ch = 3 carry zero weights), so
+//     an MFMA K-step is one kernel row and a lane's 8 k-values are two
+//     horizontally adjacent input pixels: one aligned 16-B ds_read;
+//   * weights (PERM32 row order, [64][256] bf16) live in VGPRs for the whole
+//     launch (4 channel fragments x 7 K-steps);
+//   * epilogue: BN + activation -> bf16 stem tile in LDS (-inf outside the
+//     stem map, i.e. max-pool padding), then the 3x3/s2 max, 16-B stores.
+// Results equal the unfused path up to fp32 summation order inside the conv
+// (the max-pool is exact on the same bf16 values).
+#include "rr_internal.h"
+
+namespace rr {
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 tbf16x8_t;
+typedef __attribute__((ext_vector_type(4))) float tf32x4_t;
+
+struct StemArgs {
+    const float* x;   // [n][3][h][w]
+    const uint4* w;   // [64][256] bf16 (as 16-B chunks), PERM32 rows, k = kh*32 + kw*4 + ci
+    const float* scale;
+    const float* shift;
+    bf16_t* y;        // [n][hp][wp][64]
+    int n, h, w_, ho, wo, hp, wp;
+    float mean[3], stdv[3];
+    int do_norm, leaky;
+    float slope;
+};
+
+constexpr int NT = 512;  // threads per block (8 waves)
+
+template <int PH, int PW>
+__global__ void __launch_bounds__(NT) k_stem_pool(StemArgs a, int tiles_w, int tiles_hw, int ntiles) {
+    constexpr int SR = 2 * PH + 1, SC = 2 * PW + 1, NP = SR * SC, NF = (NP + 15) / 16;
+    constexpr int IR = 2 * (SR - 1) + 7, IC = 2 * (SC - 1) + 8;  // IC even: 16-B aligned pixel pairs
+    constexpr int NSLOT = IR * IC, SPT = (NSLOT + NT - 1) / NT;
+    constexpr int PATCH = NSLOT * 8;
+    static_assert(IC % 2 == 0, "pixel pairs");
+    __shared__ __attribute__((aligned(16))) char sP[2][PATCH];
+    __shared__ __attribute__((aligned(16))) char sO[NF * 16 * 128];
+    __shared__ __attribute__((aligned(16))) float sS[64], sH[64];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r16 = lane & 15, q = lane >> 4;
+    const int H = a.h, W = a.w_;
+    const long long plane = (long long)H * W;
+
+    if (tid < 64) {
+        sS[tid] = a.scale[tid];
+        sH[tid] = a.shift[tid];
+    }
+    // weights -> VGPRs: fragment i (packed rows 16i..16i+15), K-step m
+    uint4 areg[4][7];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int m = 0; m < 7; ++m) areg[i][m] = a.w[(i * 16 + r16) * 32 + m * 4 + q];
+
+    auto tile_origin = [&](int t, int& img, int& ph0, int& pw0) {
+        img = t / tiles_hw;
+        const int rem = t - img * tiles_hw;
+        const int th = rem / tiles_w;
+        ph0 = th * PH;
+        pw0 = (rem - th * tiles_w) * PW;
+    };
+
+    float pf[SPT][3];
+    auto fill_load = [&](int t) {
+        int img, ph0, pw0;
+        tile_origin(t, img, ph0, pw0);
+        const int ir0 = 4 * ph0 - 5, ic0 = 4 * pw0 - 5;  // = 2 * (2 * p0 - 1) - 3
+        const float* src = a.x + (long long)img * 3 * plane;
+#pragma unroll
+        for (int u = 0; u < SPT; ++u) {
+            const int slot = tid + NT * u;
+            const int r = slot / IC, c = slot - r * IC;
+            const int ih = ir0 + r, iw = ic0 + c;
+            const bool ok = slot < NSLOT && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+            const long long o = ok ? (long long)ih * W + iw : 0;
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) pf[u][ch] = ok ? src[ch * plane + o] : 0.f;
+        }
+    };
+    auto fill_store = [&](int t, int buf) {
+        int img, ph0, pw0;
+        tile_origin(t, img, ph0, pw0);
+        const int ir0 = 4 * ph0 - 5, ic0 = 4 * pw0 - 5;
+#pragma unroll
+        for (int u = 0; u < SPT; ++u) {
+            const int slot = tid + NT * u;
+            if (slot >= NSLOT) continue;
+            const int r = slot / IC, c = slot - r * IC;
+            const bool ok = (unsigned)(ir0 + r) < (unsigned)H && (unsigned)(ic0 + c) < (unsigned)W;
+            float v[3];
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch)  // zero padding is applied AFTER normalisation
+                v[ch] = (ok && a.do_norm) ? (pf[u][ch] - a.mean[ch]) / a.stdv[ch] : pf[u][ch];
+            uint2 o;
+            o.x = pack_bf16x2(v[0], v[1]);
+            o.y = pack_bf16x2(v[2], 0.f);
+            *reinterpret_cast<uint2*>(sP[buf] + slot * 8) = o;
+        }
+    };
+
+    int t = blockIdx.x;
+    if (t >= ntiles) return;
+    fill_load(t);
+    fill_store(t, 0);
+    __syncthreads();
+    int cur = 0;
+    for (; t < ntiles; t += gridDim.x, cur ^= 1) {
+        const int tn = t + gridDim.x;
+        if (tn < ntiles) fill_load(tn);
+        int img, ph0, pw0;
+        tile_origin(t, img, ph0, pw0);
+        const int sr0 = 2 * ph0 - 1, sc0 = 2 * pw0 - 1;
+        const char* patch = sP[cur];
+        for (int f = wave; f < NF; f += NT / 64) {
+            const int n = f * 16 + r16;
+            const int nn = n < NP ? n : NP - 1;
+            const int sr = nn / SC, sc = nn - sr * SC;
+            const char* pb = patch + ((2 * sr) * IC + 2 * sc + 2 * q) * 8;
+            tf32x4_t acc[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[i] = (tf32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int m = 0; m < 7; ++m) {
+                const uint4 b = *reinterpret_cast<const uint4*>(pb + m * IC * 8);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(tbf16x8_t, areg[i][m]),
+                                                                    __builtin_bit_cast(tbf16x8_t, b), acc[i], 0, 0, 0);
+            }
+            const bool valid = (unsigned)(sr0 + sr) < (unsigned)a.ho && (unsigned)(sc0 + sc) < (unsigned)a.wo;
+            if (n < NP) {
+#pragma unroll
+                for (int i2 = 0; i2 < 2; ++i2) {
+                    const int cl = 32 * i2 + 8 * q;  // 8 consecutive channels (PERM32 rows)
+                    float v[8];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        v[r] = acc[2 * i2][r] * sS[cl + r] + sH[cl + r];
+                        v[4 + r] = acc[2 * i2 + 1][r] * sS[cl + 4 + r] + sH[cl + 4 + r];
+                    }
+                    if (a.leaky) {
+#pragma unroll
+                        for (int r = 0; r < 8; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * a.slope;
+                    }
+                    uint4 o;
+                    if (valid) {
+                        o.x = pack_bf16x2(v[0], v[1]);
+                        o.y = pack_bf16x2(v[2], v[3]);
+                        o.z = pack_bf16x2(v[4], v[5]);
+                        o.w = pack_bf16x2(v[6], v[7]);
+                    } else {
+                        o = make_uint4(0xFF80FF80u, 0xFF80FF80u, 0xFF80FF80u, 0xFF80FF80u);  // -inf: pool padding
+                    }
+                    const int chunk = 4 * i2 + q;
+                    *reinterpret_cast<uint4*>(sO + n * 128 + ((chunk ^ (n & 7)) << 4)) = o;
+                }
+            }
+        }
+        if (tn < ntiles) fill_store(tn, cur ^ 1);
+        __syncthreads();
+        // 3x3 / s2 max over the stem tile; item = (pooled pixel, 8-channel chunk)
+#pragma unroll
+        for (int it = 0; it < (PH * PW * 8 + NT - 1) / NT; ++it) {
+            const int item = tid + NT * it;
+            if (item >= PH * PW * 8) break;
+            const int c = item & 7, pp = item >> 3;
+            const int pr = pp / PW, pc = pp - pr * PW;
+            if (ph0 + pr >= a.hp || pw0 + pc >= a.wp) continue;
+            float mx[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) mx[j] = -__builtin_inff();
+#pragma unroll
+            for (int dr = 0; dr < 3; ++dr)
+#pragma unroll
+                for (int dc = 0; dc < 3; ++dc) {
+                    const int n = (2 * pr + dr) * SC + 2 * pc + dc;
+                    const uint4 v = *reinterpret_cast<const uint4*>(sO + n * 128 + ((c ^ (n & 7)) << 4));
+                    const unsigned w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        mx[2 * j] = fmaxf(mx[2 * j], __uint_as_float(w4[j] << 16));
+                        mx[2 * j + 1] = fmaxf(mx[2 * j + 1], __uint_as_float(w4[j] & 0xffff0000u));
+                    }
+                }
+            uint4 o;
+            o.x = pack_bf16x2(mx[0], mx[1]);
+            o.y = pack_bf16x2(mx[2], mx[3]);
+            o.z = pack_bf16x2(mx[4], mx[5]);
+            o.w = pack_bf16x2(mx[6], mx[7]);
+            *reinterpret_cast<uint4*>(a.y + (((long long)img * a.hp + ph0 + pr) * a.wp + pw0 + pc) * 64 + 8 * c) = o;
+        }
+        __syncthreads();
+    }
+}
+
+// out[R][k], R packed row (PERM32), k = kh*32 + kw*4 + ci (kh < 7, kw < 7, ci < 3 real; rest 0)
+__global__ void k_stem_pack(const float* __restrict__ w, bf16_t* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= 64 * 256) return;
+    const int R = i >> 8, k = i & 255;
+    const int co = perm32_channel(R);
+    const int kh = k >> 5, kw = (k >> 2) & 7, ci = k & 3;
+    float v = 0.f;
+    if (kh < 7 && kw < 7 && ci < 3) v = w[((co * 3 + ci) * 7 + kh) * 7 + kw];
+    out[i] = f2bf(v);
+}
+
+int g_stem_cus = 0;
+
+}  // namespace
+
+}  // namespace rr
+
+using namespace rr;
+
+extern "C" int rr_stem_pack_weights(const float* w, int c_out, int c_in, int kh, int kw, void* out, void* stream) {
+    if (!w || !out) return fail(RR_EINVAL, "rr_stem_pack_weights: null pointer");
+    if (c_out != 64 || c_in != 3 || kh != 7 || kw != 7)
+        return fail(RR_EINVAL, "rr_stem_pack_weights: the fused stem is the 3->64 7x7 conv1");
+    hipLaunchKernelGGL(k_stem_pack, dim3(64), dim3(256), 0, as_stream(stream), w, (bf16_t*)out);
+    return check_launch("rr_stem_pack_weights");
+}
+
+extern "C" int rr_stem_conv_pool(const float* x, int n, int h, int w, const float* mean_host, const float* std_host,
+                                 int do_normalize, const void* wpk, const float* scale, const float* shift, int act,
+                                 float slope, void* y, int hp, int wp, void* stream) {
+    if (!x || !wpk || !scale || !shift || !y) return fail(RR_EINVAL, "rr_stem_conv_pool: null pointer");
+    if (n <= 0 || h <= 0 || w <= 0) return fail(RR_EINVAL, "rr_stem_conv_pool: bad shape");
+    const int ho = (h + 2 * 3 - 7) / 2 + 1, wo = (w + 2 * 3 - 7) / 2 + 1;
+    if (ho <= 0 || wo <= 0) return fail(RR_EINVAL, "rr_stem_conv_pool: image smaller than the kernel");
+    if (hp != (ho + 2 - 3) / 2 + 1 || wp != (wo + 2 - 3) / 2 + 1)
+        return fail(RR_EINVAL, "rr_stem_conv_pool: output size must be the 3x3/s2/p1 pool of the stem map");
+    if ((long long)n * 3 * h * w >= (1ll << 40)) return fail(RR_EINVAL, "rr_stem_conv_pool: input too large");
+    if (act != RR_ACT_IDENTITY && act != RR_ACT_LEAKY) return fail(RR_EINVAL, "rr_stem_conv_pool: act");
+    StemArgs a;
+    a.x = x;
+    a.w = (const uint4*)wpk;
+    a.scale = scale;
+    a.shift = shift;
+    a.y = (bf16_t*)y;
+    a.n = n; a.h = h; a.w_ = w; a.ho = ho; a.wo = wo; a.hp = hp; a.wp = wp;
+    a.do_norm = do_normalize ? 1 : 0;
+    for (int c = 0; c < 3; ++c) {
+        a.mean[c] = do_normalize ? mean_host[c] : 0.f;
+        a.stdv[c] = do_normalize ? std_host[c] : 1.f;
+    }
+    a.leaky = act == RR_ACT_LEAKY;
+    a.slope = slope;
+    constexpr int PH = 4, PW = 32;
+    const int tiles_w = (wp + PW - 1) / PW, tiles_h = (hp + PH - 1) / PH;
+    const long long ntiles = (long long)n * tiles_h * tiles_w;
+    if (ntiles >= (1ll << 31)) return fail(RR_EINVAL, "rr_stem_conv_pool: too many tiles");
+    if (g_stem_cus == 0) {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 256;
+        g_stem_cus = cus;
+    }
+    const int grid = (int)(ntiles < g_stem_cus ? ntiles : g_stem_cus);
+    hipLaunchKernelGGL((k_stem_pool<PH, PW>), dim3(grid), dim3(NT), 0, as_stream(stream), a, tiles_w,
+                       tiles_w * tiles_h, (int)ntiles);
+    return check_launch("rr_stem_conv_pool");
+}

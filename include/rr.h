@@ -96,6 +96,19 @@ int rr_pack_conv_weights(const float* w, int c_out, int c_in, int kh, int kw, in
 int rr_maxpool2d(const void* x, int n, int h, int w, int c, int k, int stride, int pad,
                  void* y, int ho, int wo, int dtype, void* stream);
 
+/* Fused ResNet stem, bf16: normalise + conv1 7x7/s2/p3 (3 -> 64) + BN affine
+ * + activation + max-pool 3x3/s2/p1 in one kernel.  Replaces mod1 =
+ * Sequential(conv1, bn1, pool1) of cirtorch/backbones/resnet.py:59-66 applied
+ * to the output of utils/image.py:125 `normalize`.
+ *   x     : [n][3][h][w] float32 (raw pixels when do_normalize, mean/std HOST arrays of 3)
+ *   wpk   : rr_stem_pack_weights output, bf16 [64][256]
+ *   scale, shift : [64] float32 (folded BN), act RR_ACT_*, slope for leaky
+ *   y     : [n][hp][wp][64] bf16, hp/wp = the pool of the (h+1)/2 x (w+1)/2 stem map */
+int rr_stem_pack_weights(const float* w, int c_out, int c_in, int kh, int kw, void* out, void* stream);
+int rr_stem_conv_pool(const float* x, int n, int h, int w, const float* mean_host, const float* std_host,
+                      int do_normalize, const void* wpk, const float* scale, const float* shift, int act,
+                      float slope, void* y, int hp, int wp, void* stream);
+
 /* Bilinear resize, align_corners=False, NCHW float32 (one image).
  * Replaces nn.functional.interpolate(scale_factor=s, mode='bilinear',
  * align_corners=False) of the multi-scale pyramid (cirtorch/models/GF_net.py:32-35). */

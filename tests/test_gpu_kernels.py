@@ -199,3 +199,39 @@ def test_whitenapply_vs_reference_golden(cuda):
     np.testing.assert_allclose(Y, g["Y32"], rtol=1e-4, atol=2e-6)
     Yf = whitenapply(X, g["m"].astype(np.float32), g["P"].astype(np.float32))
     assert cosines(Yf, g["Y"]).min() > 1 - 1e-5
+
+
+@pytest.mark.parametrize("shape", [(2, 61, 83), (1, 96, 128), (1, 40, 300)])
+@pytest.mark.parametrize("norm", [True, False])
+def test_stem_conv_pool(cuda, shape, norm):
+    """Fused normalise + conv1 7x7/s2/p3 + BN + leaky + maxpool 3x3/s2/p1
+    (cirtorch/backbones/resnet.py:59-66) against an fp64 restatement on the
+    same bf16-rounded operands, and against the unfused engine path."""
+    n, h, w = shape
+    g = torch.Generator().manual_seed(h * 1000 + w)
+    x = torch.rand(n, 3, h, w, generator=g)
+    wt = _bf16_round(torch.randn(64, 3, 7, 7, generator=g) * 0.1)
+    scale = torch.rand(64, generator=g) + 0.5
+    shift = torch.randn(64, generator=g) * 0.1
+    mean, std = ([0.485, 0.456, 0.406], [0.229, 0.224, 0.225]) if norm else (None, None)
+    ops = _ops()
+    wpk = ops.pack_stem_weights(wt.to(cuda))
+    got = ops.stem_conv_pool(x.to(cuda), wpk, scale.to(cuda), shift.to(cuda), leaky=True, slope=0.01,
+                             mean=mean, std=std).float().cpu()
+    xn = x if not norm else (x - torch.tensor(mean)[:, None, None]) / torch.tensor(std)[:, None, None]
+    xn = _bf16_round(xn)
+    ref = F.conv2d(xn.double(), wt.double(), stride=2, padding=3) * scale.double()[None, :, None, None] \
+        + shift.double()[None, :, None, None]
+    ref = _bf16_round(F.leaky_relu(ref, 0.01).float())
+    ref = F.max_pool2d(ref, 3, 2, 1).permute(0, 2, 3, 1)
+    assert got.shape == ref.shape
+    err = (got - ref).abs().max().item()
+    assert err <= 8e-3 * ref.abs().max().item(), err
+    # unfused engine path on the same inputs
+    xe = ops.image_to_nhwc(x.to(cuda), 8, torch.bfloat16, mean, std)
+    wp = ops.pack_conv_weights(wt.to(cuda), 8, torch.bfloat16, perm32=True)
+    y = ops.conv2d_fused(xe, wp, 7, 7, 2, 3, 64, scale.to(cuda), shift.to(cuda), leaky=True, perm32=True)
+    un = ops.maxpool2d(y, 3, 2, 1).float().cpu()
+    assert (got - un).abs().max().item() <= 8e-3 * ref.abs().max().item()
+    # most values are bit-identical (only fp32 summation order differs)
+    assert (got == un).float().mean().item() > 0.95
