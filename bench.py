@@ -44,7 +44,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=32, help="images per rank per step")
+    ap.add_argument("--batch", type=int, default=128, help="images (= queries) per rank per step")
+    ap.add_argument("--extract-batch", type=int, default=32,
+                    help="images per extractor launch chain (the step's batch runs as batch/extract-batch chains)")
     ap.add_argument("--height", type=int, default=768)
     ap.add_argument("--width", type=int, default=1024)
     ap.add_argument("--arch", default="resnet50")
@@ -86,6 +88,40 @@ def conv_flops_per_image(body, h, w):
                 cv = blk.proj_conv
                 tot += 2 * out(h0, 1, cv.stride[0], 0) * out(w0, 1, cv.stride[0], 0) * cv.out_channels * cv.in_channels
     return tot
+
+
+def layer_costs(body, h, w, esz=2):
+    """Per-layer algorithmic (FLOPs, HBM bytes) of one image through the body:
+    each conv reads its input map and (conv3) the residual once and writes its
+    output once (esz bytes per activation); the fused stem reads the float32
+    image and writes the pooled map.  Used for the layer-resolved roofline
+    floor sum_l max(flops_l / peak_mfma, bytes_l / peak_hbm)."""
+    def out(s, k, st, p):
+        return (s + 2 * p - k) // st + 1
+    costs = []
+    c = body.mod1.conv1
+    hh, ww = out(h, 7, 2, 3), out(w, 7, 2, 3)
+    hp, wp = out(hh, 3, 2, 1), out(ww, 3, 2, 1)
+    costs.append((2 * hh * ww * c.out_channels * c.in_channels * 49, h * w * 3 * 4 + hp * wp * 64 * esz))
+    hh, ww = hp, wp
+    for m in range(2, 6):
+        for blk in getattr(body, "mod%d" % m).children():
+            convs = [blk.convs.conv1, blk.convs.conv2] + ([blk.convs.conv3] if blk.is_bottleneck else [])
+            h0, w0, c0 = hh, ww, convs[0].in_channels
+            for i, cv in enumerate(convs):
+                k, st, p = cv.kernel_size[0], cv.stride[0], cv.padding[0]
+                hi, wi = hh, ww
+                hh, ww = out(hh, k, st, p), out(ww, k, st, p)
+                nout = hh * ww * cv.out_channels * esz
+                res = nout if i == len(convs) - 1 else 0
+                costs.append((2 * hh * ww * cv.out_channels * cv.in_channels * k * k,
+                              hi * wi * cv.in_channels * esz + nout + res))
+            if hasattr(blk, "proj_conv"):
+                cv = blk.proj_conv
+                ho, wo = out(h0, 1, cv.stride[0], 0), out(w0, 1, cv.stride[0], 0)
+                costs.append((2 * ho * wo * cv.out_channels * cv.in_channels,
+                              ho * wo * c0 * esz + ho * wo * cv.out_channels * esz))
+    return costs
 
 
 def cpu_baseline(args):
@@ -160,17 +196,26 @@ def main():
             q = qa
         return index.search(q, args.k)
 
+    EB = max(1, min(args.extract_batch, B))
+
+    def extract_all(record):
+        """the step's B images as B/EB extractor chains -> D x B descriptors"""
+        descs = []
+        for c in range(0, B, EB):
+            if record:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(main_stream)
+            descs.append(net.extract(images[c:c + EB]))
+            if record:
+                e1.record(main_stream)
+                ev_pairs.append((e0, e1))
+        return descs[0] if len(descs) == 1 else torch.cat(descs, dim=1)
+
     def step(record):
-        """extract batch i on the main stream; its match (memory-bound kNN +
-        RCCL) runs on a second stream, overlapping batch i+1's extraction."""
-        e0 = e1 = None
-        if record:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(main_stream)
-        desc = net.extract(images)                  # D x B (on-device, fp32)
-        if record:
-            e1.record(main_stream)
-            ev_pairs.append((e0, e1))
+        """extract the step's images on the main stream, then one top-k search
+        of all of them; with --overlap the match (memory-bound kNN + RCCL) runs
+        on a second stream, overlapping the next step's extraction."""
+        desc = extract_all(record)                  # D x B (on-device, fp32)
         if match_stream is main_stream:
             return match(desc)
         ready = torch.cuda.Event()
@@ -197,13 +242,13 @@ def main():
             t = torch.tensor([elapsed], device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
-        body_ms = sum(a.elapsed_time(b) for a, b in ev_pairs) / len(ev_pairs)
+        body_ms = sum(a.elapsed_time(b) for a, b in ev_pairs) / args.steps   # extractor time per step
 
         # extract-only loop (same net, no matching)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         for _ in range(max(3, args.steps // 2)):
-            net.extract(images)
+            extract_all(False)
         torch.cuda.synchronize()
         ext_only = max(3, args.steps // 2) * B / (time.perf_counter() - t1)
 
@@ -235,6 +280,10 @@ def main():
                                 "note": "per-rank screening GEMM FLOPs 2*Q*n_local*D / whole search time"}}
 
     fl_img = conv_flops_per_image(net.body, H, W)
+    costs = layer_costs(net.body, H, W, 2 if args.precision == "bf16" else 4)
+    peak_m = (PEAK_BF16_TFLOPS if args.precision == "bf16" else PEAK_F32_TFLOPS) * 1e12
+    floor_ms = B * sum(max(f / peak_m, b / (PEAK_HBM_GBS * 1e9)) for f, b in costs) * 1e3
+    bytes_img = sum(b for _, b in costs)
     achieved = fl_img * B / (body_ms * 1e-3) / 1e12
     peak = PEAK_BF16_TFLOPS if args.precision == "bf16" else PEAK_F32_TFLOPS
     value = world * B * args.steps / elapsed
@@ -251,15 +300,22 @@ def main():
         "vs_baseline": None,
         "dtype": args.precision,
         "data": "synthetic (U[0,1) images, random-init weights, counter-hash N(0,1) unit DB rows)",
-        "config": {"workload": "%s-GeM+whiten %s extract %dx%d, B=%d/GPU, then top-%d cosine kNN of all %d queries "
-                               "vs %d x %d DB sharded over %d GPU(s)" % (args.arch, args.precision, W, H, B, args.k,
-                                                                        B * world, args.db_rows, args.dim, world),
-                   "global_batch": B * world, "image": [3, H, W], "db_rows": args.db_rows, "dim": args.dim,
+        "config": {"workload": "%s-GeM+whiten %s extract %dx%d, B=%d/GPU (chains of %d), then top-%d cosine kNN of "
+                               "all %d queries vs %d x %d DB sharded over %d GPU(s)"
+                               % (args.arch, args.precision, W, H, B, EB, args.k, B * world, args.db_rows, args.dim,
+                                  world),
+                   "global_batch": B * world, "extract_batch": EB, "image": [3, H, W], "db_rows": args.db_rows,
+                   "dim": args.dim,
                    "k": args.k, "parallelism": "dp%d (images) x db-shard%d" % (world, world)},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                      "frac": achieved / peak, "traffic": None,
                      "note": "dominant kernel = k_conv (implicit-GEMM MFMA conv family, 53 launches/forward); "
                              "%.2f GFLOP/img x %d img / extract-body event time %.3f ms" % (fl_img / 1e9, B, body_ms)},
+        "roofline_layers": {"floor_ms": floor_ms, "measured_ms": body_ms, "frac": floor_ms / body_ms,
+                            "hbm_bytes_per_img": bytes_img, "peak_mfma_tflops": peak_m / 1e12,
+                            "peak_hbm_gbs": PEAK_HBM_GBS,
+                            "note": "sum over the body's 53 conv layers of max(FLOPs/peak_mfma, algorithmic HBM bytes/"
+                                    "peak_hbm) for the step's images, over the measured extractor time"},
         "extract_images_per_sec": ext_only * world,
         "knn": knn,
     }

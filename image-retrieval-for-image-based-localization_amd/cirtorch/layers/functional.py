@@ -12,11 +12,24 @@ from .. import _engine as E
 from .. import _ops
 
 
+_P_CACHE = {}
+
+
 def _p_value(p):
+    """Host value of the GeM exponent.  A GPU parameter is read back once per
+    version (``Tensor._version`` bumps on every in-place update, e.g.
+    ``load_state_dict``), so steady-state forwards issue no device->host sync
+    (which would drain the stream and break HIP-graph capture)."""
     if torch.is_tensor(p):
         if p.numel() != 1:
             raise NotImplementedError("per-channel GeM exponents (GeMmp) are out of scope")
-        return float(p.detach().reshape(-1)[0].item())
+        key = (p.data_ptr(), p.device, p._version)
+        v = _P_CACHE.get(key)
+        if v is None:
+            if len(_P_CACHE) > 64:
+                _P_CACHE.clear()
+            v = _P_CACHE[key] = float(p.detach().reshape(-1)[0].item())
+        return v
     return float(p)
 
 

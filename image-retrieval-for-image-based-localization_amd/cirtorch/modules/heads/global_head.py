@@ -9,6 +9,7 @@ head tail (``rr_head_l2n_whiten_l2n``).
 import torch.nn as nn
 
 from ... import _ops
+from ...layers import functional as LF
 from ...layers.normalization import L2N
 from ...layers.pooling import GeM, MAC, SPoC
 from ..abn import ABN
@@ -41,7 +42,7 @@ class globalHead(nn.Module):
         """[N, C, h, w] -> [N, C] float32 (one launch)."""
         from ... import _engine as E
         if isinstance(self.pool, GeM):
-            return _ops.global_pool(x, E.RR_POOL_GEM, float(self.pool.p.detach().reshape(-1)[0].item()), self.pool.eps)
+            return _ops.global_pool(x, E.RR_POOL_GEM, LF._p_value(self.pool.p), self.pool.eps)
         if isinstance(self.pool, MAC):
             return _ops.global_pool(x, E.RR_POOL_MAC)
         if isinstance(self.pool, SPoC):

@@ -298,7 +298,9 @@ static void launch(const ConvArgs& a, bool k1, hipStream_t s) {
 
 template <typename T, typename TO> void launch_gemm2(const ConvArgs& a, bool k1, hipStream_t s);
 bool launch_stream1x1(const ConvArgs& a, hipStream_t s);  // rr_stream.hip
+bool launch_conv3x3(const ConvArgs& a, hipStream_t s);    // rr_conv3.hip
 extern int g_stream_mode;
+extern int g_conv3_mode;
 
 // out[R][k] = w[chan(R)][ci][kh][kw] with k = (kh*KW + kw)*cin_pad + ci, zeros elsewhere.
 template <typename T>
@@ -334,6 +336,7 @@ template <typename T, typename TO>
 static void dispatch(const ConvArgs& a, bool k1, int dtype, hipStream_t s) {
     if constexpr (sizeof(T) == 2 && sizeof(TO) == 2) {
         if (k1 && launch_stream1x1(a, s)) return;
+        if (!k1 && launch_conv3x3(a, s)) return;
     }
     if (use_v2(a, dtype)) launch_gemm2<T, TO>(a, k1, s);
     else launch<T, TO>(a, k1, s);
@@ -406,8 +409,9 @@ namespace rr {
 void set_gemm_tuning(int key, int value);
 }
 extern "C" int rr_set_tuning(int key, int value) {
-    if (key < 0 || key > 5) return fail(RR_EINVAL, "rr_set_tuning: unknown key");
+    if (key < 0 || key > 6) return fail(RR_EINVAL, "rr_set_tuning: unknown key");
     if (key == RR_TUNE_STREAM_1X1) rr::g_stream_mode = value;
+    else if (key == RR_TUNE_CONV3X3) rr::g_conv3_mode = value;
     else rr::set_gemm_tuning(key, value);
     return RR_OK;
 }

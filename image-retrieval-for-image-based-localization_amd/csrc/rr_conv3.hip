@@ -1,0 +1,356 @@
+// librr.so — direct 3x3 convolution (stride 1, pad 1, bf16) with the input
+// halo patch staged ONCE in LDS.
+//
+// The implicit-GEMM engine (rr_gemm.hip) stages an im2col B tile per K-step,
+// so every input pixel crosses the L2 -> LDS path 9 times (once per tap): the
+// 3x3 layers of the bottleneck blocks run at 50-100 FLOP per staged byte and
+// are bound by that path, not by the matrix cores.  Here a block owns an
+// output tile of TH x TW pixels of one image x TC output channels; per
+// 64-channel input chunk it stages the (TH+2) x (TW+2) halo patch once and
+// reads the 9 taps out of LDS by address offset (6x fewer staged bytes at
+// 8 x 32 tiles).  With 64 input channels the block's whole weight slice
+// (9 taps x TC rows x 128 B) also stays resident in LDS ("A-stationary");
+// otherwise the 128-B weight K-steps stream through a 2-stage ring and the
+// next chunk's patch is fetched one 1-KiB piece per tap behind them.
+//
+// K order per output tile: (input chunk cc, tap, 64 channels).  The standard
+// packed weight row (k = tap*c_in + ci, RR_CONV_PERM32 rows) is read at
+// k0 = tap*c_in + cc*64, so no special packing is needed.
+// LDS images: weight K-step [TC rows][128 B], patch [pixel][128 B]; both with
+// the 16-B chunk XOR swizzle (chunk ^ (row & 7)) applied on the DMA source, so
+// every ds_read_b128 lane group of a fragment read hits distinct slots.
+// Synchronisation: LDS-DMA (buffer_load ... lds) tracked by counted vmcnt +
+// raw s_barrier; the epilogue reads BN scale/shift from LDS, so no
+// compiler-visible global load ever drains the DMA queue.
+//
+// Replaces the 3x3 nn.Conv2d of ResidualBlock (cirtorch/backbones/misc.py:
+// 166-172, stride on this conv; here the stride-1 blocks) + the ABN eval BN +
+// leaky_relu (cirtorch/utils/misc.py:175-235).
+#include "rr_internal.h"
+
+namespace rr {
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 pbf16x8_t;
+typedef __attribute__((ext_vector_type(4))) float pf32x4_t;
+typedef __attribute__((ext_vector_type(4))) int pi32x4_t;
+
+constexpr unsigned POOB = 0x80000000u;  // voffset beyond every buffer: the DMA writes zeros
+
+// One 16-B-per-lane LDS-DMA wave-instruction: LDS[lds_addr + lane*16] = buf[voff].
+__device__ __forceinline__ void pdma16(pi32x4_t rsrc, unsigned voff, unsigned lds_addr) {
+    unsigned keep;
+    lds_addr = __builtin_amdgcn_readfirstlane(lds_addr);
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %3\n\t"
+        "s_nop 4\n\t"
+        "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(rsrc), "s"(lds_addr)
+        : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void pwait_barrier() {
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"(N) : "memory");
+}
+
+__device__ __forceinline__ pi32x4_t prsrc(const void* base, unsigned bytes) {
+    const unsigned long long b = (unsigned long long)base;
+    pi32x4_t r;
+    r.x = __builtin_amdgcn_readfirstlane((int)(unsigned)b);
+    r.y = __builtin_amdgcn_readfirstlane((int)((unsigned)(b >> 32) & 0xFFFFu));
+    r.z = __builtin_amdgcn_readfirstlane((int)bytes);
+    r.w = 0x00020000;
+    return r;
+}
+
+struct TileC {
+    int ct, img, oh0, ow0;
+};
+
+template <int TC, int TH, int TW, int WC, int WP, bool ARES>
+__global__ void __launch_bounds__(64 * WC * WP) k_conv3x3(ConvArgs a, int tiles_w, int tiles_hw, int tiles_c,
+                                                         int ntiles) {
+    constexpr int NW = WC * WP, NT = 64 * NW;
+    constexpr int TP = TH * TW;
+    constexpr int PC = TW + 2, NPIX = (TH + 2) * PC;
+    constexpr int NDP = (NPIX + 7) / 8;          // patch wave-instructions (8 pixels x 128 B each)
+    constexpr int NDPW = (NDP + NW - 1) / NW;    // ... per wave (ring mode: one per tap)
+    constexpr int PBYTES = (ARES ? NDP : NDPW * NW) * 1024;
+    constexpr int NIA = TC / (8 * NW);           // weight wave-instructions per wave per K-step
+    constexpr int AST = TC * 128;                // one weight K-step in LDS
+    constexpr int ABYTES = (ARES ? 9 : 2) * AST;
+    constexpr int MAXC = ARES ? TC : 512;        // BN scale/shift of every output channel
+    constexpr int FM = TC / WC / 16, FN = TP / WP / 16;
+    constexpr int NST = (FM / 2) * FN;           // epilogue stores per wave (full tiles only)
+    static_assert(TC % (8 * NW) == 0 && FM % 2 == 0 && TW % 16 == 0 && (TP / WP) % 16 == 0, "tile shape");
+    static_assert(ARES || NDPW <= 8, "ring mode fetches the next patch one piece per tap (taps 0..7)");
+    static_assert(NST >= 2, "vmcnt immediates below assume NST > 1");
+    __shared__ __attribute__((aligned(1024))) char smem[ABYTES + 2 * PBYTES + 2 * MAXC * 4];
+    float* sS = reinterpret_cast<float*>(smem + ABYTES + 2 * PBYTES);
+    float* sH = sS + MAXC;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wc = wave % WC, wp = wave / WC;
+    const int H = a.h, W = a.w_, Cin = a.cin, nck = Cin >> 6;
+    const pi32x4_t rsX = prsrc(a.x, (unsigned)((long long)a.n * H * W * Cin * 2));
+    const unsigned lds0 = (unsigned)(unsigned long long)smem;
+    const int lrow = lane >> 3, lch = lane & 7;
+
+    {
+        const bool aff = a.flags & RR_CONV_AFFINE;
+        for (int i = tid; i < a.cout; i += NT) {
+            sS[i] = aff ? a.scale[i] : 1.f;
+            sH[i] = aff ? a.shift[i] : 0.f;
+        }
+    }
+    const int my_tiles = (int)blockIdx.x < ntiles ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+    if (my_tiles == 0) return;
+
+    auto tile_of = [&](int lt) {
+        const int t = (int)blockIdx.x + lt * (int)gridDim.x;
+        TileC c;
+        c.ct = t % tiles_c;
+        const int pt = t / tiles_c;
+        c.img = pt / tiles_hw;
+        const int rem = pt - c.img * tiles_hw;
+        const int th = rem / tiles_w;
+        c.oh0 = th * TH;
+        c.ow0 = (rem - th * tiles_w) * TW;
+        return c;
+    };
+
+    // wave-instruction d of the patch of (tile, chunk cc) -> patch buffer `buf`:
+    // patch pixels 8d .. 8d+7 (origin (oh0-1, ow0-1)); outside the image -> zeros
+    auto patch_dma = [&](TileC tc, int cc, int buf, int d) {
+        const int q = d * 8 + lrow;
+        const int pr = q / PC, pc = q - pr * PC;
+        const int hh = tc.oh0 - 1 + pr, ww = tc.ow0 - 1 + pc;
+        unsigned off = POOB;
+        if (q < NPIX && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W)
+            off = (unsigned)(((((long long)tc.img * H + hh) * W + ww) * Cin + cc * 64 + ((lch ^ lrow) << 3)) * 2);
+        pdma16(rsX, off, lds0 + ABYTES + buf * PBYTES + d * 1024);
+    };
+    // weight K-step (tap, chunk cc) of channel tile ct -> LDS dst ([TC rows][128 B], swizzled)
+    auto w_dma = [&](int ct, int tap, int cc, unsigned dst) {
+        const pi32x4_t rsW = prsrc((const char*)a.w + (long long)ct * TC * a.kp * 2, (unsigned)(TC * a.kp * 2));
+        const unsigned k0b = (unsigned)((tap * Cin + cc * 64) * 2);
+#pragma unroll
+        for (int i = 0; i < NIA; ++i) {
+            const int row = (wave + NW * i) * 8 + lrow;
+            pdma16(rsW, (unsigned)(row * a.kp * 2) + k0b + (unsigned)((lch ^ lrow) << 4), dst + (wave + NW * i) * 1024);
+        }
+    };
+
+    const int r16 = lane & 15, kq = lane >> 4;
+    const int arow0 = wc * (TC / WC) + r16;
+    int bq[FN];  // patch pixel read by this lane for fragment j at tap (0, 0)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+        const int p = wp * (TP / WP) + j * 16;
+        bq[j] = (p / TW) * PC + (p % TW) + r16;
+    }
+
+    pf32x4_t acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = (pf32x4_t){0.f, 0.f, 0.f, 0.f};
+
+    auto mfma_step = [&](const char* As, const char* Ps, int toff) {
+#pragma unroll
+        for (int hs = 0; hs < 2; ++hs) {
+            const int ch = kq + 4 * hs;
+            uint4 fa[FM], fb[FN];
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+                fa[i] = *reinterpret_cast<const uint4*>(As + (arow0 + i * 16) * 128 + ((ch ^ (r16 & 7)) << 4));
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+                const int q = bq[j] + toff;
+                fb[j] = *reinterpret_cast<const uint4*>(Ps + q * 128 + ((ch ^ (q & 7)) << 4));
+            }
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int j = 0; j < FN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(pbf16x8_t, fa[i]),
+                                                                        __builtin_bit_cast(pbf16x8_t, fb[j]),
+                                                                        acc[i][j], 0, 0, 0);
+        }
+    };
+
+    bf16_t* __restrict__ Y = (bf16_t*)a.y;
+    const bool leaky = a.act == RR_ACT_LEAKY;
+    const float slope = a.slope;
+    // PERM32 rows: a lane's fragment pair (2*i2, 2*i2+1) holds 8 consecutive
+    // output channels of one pixel -> one 16-B store; exactly NST stores.
+    auto epilogue = [&](const TileC& tc) {
+#pragma unroll
+        for (int i2 = 0; i2 < FM / 2; ++i2) {
+            const int c = tc.ct * TC + wc * (TC / WC) + 32 * i2 + 8 * kq;
+            const float4 s0 = *reinterpret_cast<const float4*>(sS + c);
+            const float4 s1 = *reinterpret_cast<const float4*>(sS + c + 4);
+            const float4 h0 = *reinterpret_cast<const float4*>(sH + c);
+            const float4 h1 = *reinterpret_cast<const float4*>(sH + c + 4);
+            const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+            const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+                const int p = wp * (TP / WP) + j * 16 + r16;
+                const long long pix = ((long long)tc.img * H + tc.oh0 + p / TW) * W + tc.ow0 + p % TW;
+                float v[8];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    v[r] = acc[2 * i2][j][r] * sc[r] + sh[r];
+                    v[4 + r] = acc[2 * i2 + 1][j][r] * sc[4 + r] + sh[4 + r];
+                }
+                if (leaky) {
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * slope;
+                }
+                uint4 o;
+                o.x = pack_bf16x2(v[0], v[1]);
+                o.y = pack_bf16x2(v[2], v[3]);
+                o.z = pack_bf16x2(v[4], v[5]);
+                o.w = pack_bf16x2(v[6], v[7]);
+                *reinterpret_cast<uint4*>(Y + pix * a.ldy + c) = o;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) acc[i][j] = (pf32x4_t){0.f, 0.f, 0.f, 0.f};
+    };
+
+    TileC cur = tile_of(0);
+    if constexpr (ARES) {
+        // c_in = 64, one channel tile: weights for all 9 taps stay resident; per
+        // tile one barrier, the next tile's patch in flight during this one.
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) w_dma(0, tap, 0, lds0 + tap * AST);
+        for (int d = wave; d < NDP; d += NW) patch_dma(cur, 0, 0, d);
+        for (int lt = 0; lt < my_tiles; ++lt) {
+            // patch(lt) landed (older than the previous tile's NST epilogue stores)
+            if (lt == 0) pwait_barrier<0>();
+            else pwait_barrier<NST>();
+            if (lt + 1 < my_tiles) {
+                const TileC nxt = tile_of(lt + 1);
+                for (int d = wave; d < NDP; d += NW) patch_dma(nxt, 0, (lt + 1) & 1, d);
+            }
+            const char* Ps = smem + ABYTES + (lt & 1) * PBYTES;
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) mfma_step(smem + tap * AST, Ps, (tap / 3) * PC + tap % 3);
+            epilogue(cur);
+            if (lt + 1 < my_tiles) cur = tile_of(lt + 1);
+        }
+    } else {
+        // steps (tile, chunk, tap); weight K-steps through a 2-stage ring, one
+        // barrier per step; the next (tile, chunk) patch arrives piecewise.
+        const int total = my_tiles * nck * 9;
+        TileC nxt = my_tiles > 1 ? tile_of(1) : cur;
+        for (int d = wave; d < NDP; d += NW) patch_dma(cur, 0, 0, d);
+        w_dma(cur.ct, 0, 0, lds0);
+        int lt = 0, cc = 0, tap = 0, grp = 0, after = 0;
+        for (int s = 0; s < total; ++s) {
+            // A(s) landed: only `after` younger VMEM ops (a patch piece, the
+            // previous tile's epilogue stores) may stay in flight
+            if (after == 0) pwait_barrier<0>();
+            else if (after == 1) pwait_barrier<1>();
+            else if (after == NST) pwait_barrier<NST>();
+            else pwait_barrier<NST + 1>();
+            int ntap = tap + 1, ncc = cc, nlt = lt;
+            if (ntap == 9) {
+                ntap = 0;
+                if (++ncc == nck) { ncc = 0; ++nlt; }
+            }
+            after = 0;
+            if (s + 1 < total) w_dma(nlt == lt ? cur.ct : nxt.ct, ntap, ncc, lds0 + ((s + 1) & 1) * AST);
+            if (tap < NDPW) {  // piece `tap` of the next group's patch
+                const bool same = cc + 1 < nck;
+                if (same || lt + 1 < my_tiles) {
+                    TileC g;  // field-wise select (a selected reference would live in scratch)
+                    g.ct = same ? cur.ct : nxt.ct;
+                    g.img = same ? cur.img : nxt.img;
+                    g.oh0 = same ? cur.oh0 : nxt.oh0;
+                    g.ow0 = same ? cur.ow0 : nxt.ow0;
+                    patch_dma(g, same ? cc + 1 : 0, (grp + 1) & 1, wave + NW * tap);
+                    after = 1;
+                }
+            }
+            mfma_step(smem + (s & 1) * AST, smem + ABYTES + (grp & 1) * PBYTES, (tap / 3) * PC + tap % 3);
+            if (ntap == 0) {
+                ++grp;
+                if (ncc == 0) {
+                    epilogue(cur);
+                    after += NST;
+                    cur = nxt;
+                    if (nlt + 1 < my_tiles) nxt = tile_of(nlt + 1);
+                }
+            }
+            tap = ntap;
+            cc = ncc;
+            lt = nlt;
+        }
+    }
+}
+
+int g_c3_cus = 0;
+
+template <int TC, int TH, int TW, int WC, int WP, bool ARES>
+void launch_c3(const ConvArgs& a, hipStream_t s) {
+    const int tiles_w = a.w_ / TW, tiles_h = a.h / TH, tiles_c = a.cout / TC;
+    const long long ntl = (long long)a.n * tiles_h * tiles_w * tiles_c;
+    const int grid = (int)(ntl < g_c3_cus ? ntl : g_c3_cus);
+    hipLaunchKernelGGL((k_conv3x3<TC, TH, TW, WC, WP, ARES>), dim3(grid), dim3(64 * WC * WP), 0, s, a, tiles_w,
+                       tiles_w * tiles_h, tiles_c, (int)ntl);
+}
+
+}  // namespace
+
+int g_conv3_mode = 1;  // rr_set_tuning(RR_TUNE_CONV3X3): 0 off, 1 auto, 2 / 3 prefer 8x32 / 4x32 tiles
+
+// bf16 3x3 / stride 1 / pad 1 with PERM32 weights, bf16 out, no residual, and
+// image sizes the tiles divide; returns false otherwise (caller falls back to
+// the implicit-GEMM engine).
+bool launch_conv3x3(const ConvArgs& a, hipStream_t s) {
+    if (g_conv3_mode == 0) return false;
+    if (a.kh != 3 || a.kw != 3 || a.stride != 1 || a.pad != 1 || a.dil != 1) return false;
+    if (!(a.flags & RR_CONV_PERM32) || (a.flags & RR_CONV_RESIDUAL) || a.ldy != a.cout) return false;
+    if (a.cin % 64 || a.kp != 9 * a.cin || a.w_ % 32) return false;
+    if ((long long)a.n * a.h * a.w_ * a.cin * 2 >= (1ll << 31)) return false;
+    if ((long long)a.n * a.h * a.w_ >= (1ll << 31) / 2) return false;
+    if (g_c3_cus == 0) {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 256;
+        g_c3_cus = cus;
+    }
+    if (a.cin == 64 && a.cout == 64 && a.h % 8 == 0) {
+        launch_c3<64, 8, 32, 1, 4, true>(a, s);
+        return true;
+    }
+    if (a.cout % 128 == 0 && a.cout <= 512) {
+        // 8 x 32 tiles when they still give every CU two or more tiles, else 4 x 32
+        // (tuning modes 2 / 3 force one of them where the image height allows)
+        const long long t8 = a.h % 8 == 0 ? (long long)a.n * (a.h / 8) * (a.w_ / 32) * (a.cout / 128) : 0;
+        const bool want8 = g_conv3_mode == 2 || (g_conv3_mode != 3 && t8 >= 2 * g_c3_cus);
+        if (t8 > 0 && (want8 || a.h % 4 != 0)) {
+            launch_c3<128, 8, 32, 2, 4, false>(a, s);
+            return true;
+        }
+        if (a.h % 4 == 0) {
+            launch_c3<128, 4, 32, 2, 4, false>(a, s);
+            return true;
+        }
+    }
+    return false;
+}
+
+}  // namespace rr

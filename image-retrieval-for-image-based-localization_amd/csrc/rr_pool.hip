@@ -69,6 +69,65 @@ __global__ void __launch_bounds__(256) k_pool_nhwc(const T* __restrict__ x, int 
     }
 }
 
+// NHWC bf16 with c % 8 == 0 (the extractor's stage maps): one 16-B load = 8
+// channels per lane, a wave covers 512 channels of one pixel, the block's 16
+// waves split the pixels (4 loads in flight per lane); the 16 partials are
+// combined through LDS in a fixed order.  grid = (ceil(c/512), n).
+__global__ void __launch_bounds__(1024) k_pool_nhwc_bf16x8(const uint4* __restrict__ x, int c, int hw, int mode,
+                                                           float p, int ip, float eps, float* __restrict__ out) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int c8 = c >> 3;
+    const int g = blockIdx.x * 64 + lane;  // this lane's 8-channel group
+    const long long img = blockIdx.y;
+    __shared__ float part[16][512];
+    const bool mac = mode == RR_POOL_MAC;
+    float acc[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) acc[r] = mac ? -INFINITY : 0.f;
+    auto add = [&](uint4 q) {
+        const unsigned u[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float v0 = __uint_as_float(u[e] << 16), v1 = __uint_as_float(u[e] & 0xffff0000u);
+            if (mode == RR_POOL_GEM) {
+                acc[2 * e] += powp(fmaxf(v0, eps), p, ip);
+                acc[2 * e + 1] += powp(fmaxf(v1, eps), p, ip);
+            } else if (mac) {
+                acc[2 * e] = fmaxf(acc[2 * e], v0);
+                acc[2 * e + 1] = fmaxf(acc[2 * e + 1], v1);
+            } else {
+                acc[2 * e] += v0;
+                acc[2 * e + 1] += v1;
+            }
+        }
+    };
+    if (g < c8) {
+        const uint4* base = x + img * hw * c8 + g;
+        int i = wave;
+        for (; i + 48 < hw; i += 64) {
+            const uint4 q0 = base[(long long)i * c8], q1 = base[(long long)(i + 16) * c8];
+            const uint4 q2 = base[(long long)(i + 32) * c8], q3 = base[(long long)(i + 48) * c8];
+            add(q0); add(q1); add(q2); add(q3);
+        }
+        for (; i < hw; i += 16) add(base[(long long)i * c8]);
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) part[wave][lane * 8 + r] = acc[r];
+    __syncthreads();
+    if (threadIdx.x < 512) {
+        const int ch = blockIdx.x * 512 + threadIdx.x;
+        if (ch < c) {
+            float v = part[0][threadIdx.x];
+            for (int w = 1; w < 16; ++w) v = mac ? fmaxf(v, part[w][threadIdx.x]) : v + part[w][threadIdx.x];
+            if (!mac) {
+                v = v / (float)hw;
+                if (mode == RR_POOL_GEM) v = __powf(v, 1.0f / p);
+            }
+            out[img * c + ch] = v;
+        }
+    }
+}
+
 // NCHW: one wave per (image, channel) plane of hw contiguous values.
 template <typename T>
 __global__ void __launch_bounds__(256) k_pool_nchw(const T* __restrict__ x, long long planes, int hw, int mode,
@@ -110,38 +169,61 @@ __global__ void __launch_bounds__(256) k_l2n_rows(const float* __restrict__ x, i
     for (int i = threadIdx.x; i < dim; i += 256) y[row * dim + i] = xr[i] / nrm;
 }
 
-// Dense layer, one wave per output o: the wave keeps W[o][:] in registers
-// (float4 chunks lane, lane+64, ...) and streams every input row through it.
-// in_dim % 4 == 0, in_dim <= 4096.
-constexpr int LIN_MAXV = 16;  // float4 per lane -> in_dim <= 64*4*16 = 4096
-__global__ void __launch_bounds__(256) k_linear_rows(const float* __restrict__ x, int rows, int in_dim,
+// Dense layer on the exact-f32 MFMA (v_mfma_f32_16x16x4_f32): a block of 8
+// waves owns 16 outputs x 64 rows; wave w takes the K-slices kb = w, w+8, ...
+// of 16 inputs.  Lane (r = lane & 15, g = lane >> 4) loads W[o0+r][16kb+4g..+3]
+// and x[row+r][16kb+4g..+3] as float4; MFMA e of the four uses component e, so
+// each instruction sums k = 16kb + 4g + e over g — every k exactly once.  The
+// 8 partial tiles are reduced through LDS in a fixed order.  W is read once per
+// 64 rows (the old one-wave-per-output form re-read x per output: ~100x the
+// L2 traffic).  in_dim % 4 == 0.  grid = (ceil(out/16), ceil(rows/64)).
+typedef __attribute__((ext_vector_type(4))) float lf32x4_t;
+__global__ void __launch_bounds__(512) k_linear_mfma(const float* __restrict__ x, int rows, int in_dim,
                                                      const float* __restrict__ w, const float* __restrict__ b,
                                                      int out_dim, float* __restrict__ y) {
-    const int o = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (o >= out_dim) return;
-    const int n4 = in_dim / 4;
-    float4 wr[LIN_MAXV];
-    const float4* wrow = reinterpret_cast<const float4*>(w + (long long)o * in_dim);
+    constexpr int RG = 4;  // 16-row groups per block
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = lane & 15, g = lane >> 4;
+    const int o0 = blockIdx.x * 16, row0 = blockIdx.y * 16 * RG;
+    __shared__ float part[8][RG][64][4];
+    lf32x4_t acc[RG];
 #pragma unroll
-    for (int t = 0; t < LIN_MAXV; ++t) {
-        const int j = lane + 64 * t;
-        wr[t] = j < n4 ? wrow[j] : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    const float bias = b ? b[o] : 0.f;
-    for (int r = 0; r < rows; ++r) {
-        const float4* xr = reinterpret_cast<const float4*>(x + (long long)r * in_dim);
-        float s = 0.f;
+    for (int j = 0; j < RG; ++j) acc[j] = (lf32x4_t){0.f, 0.f, 0.f, 0.f};
+    const int nkb = (in_dim + 15) / 16;
+    const bool orow = o0 + r < out_dim;
+    const float* wr = w + (long long)(orow ? o0 + r : 0) * in_dim;
+    for (int kb = wave; kb < nkb; kb += 8) {
+        const int k = kb * 16 + g * 4;
+        const bool kin = k < in_dim;
+        const float4 a = (orow && kin) ? *reinterpret_cast<const float4*>(wr + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 bx[RG];
 #pragma unroll
-        for (int t = 0; t < LIN_MAXV; ++t) {
-            const int j = lane + 64 * t;
-            if (j < n4) {
-                float4 v = xr[j];
-                s += wr[t].x * v.x + wr[t].y * v.y + wr[t].z * v.z + wr[t].w * v.w;
-            }
+        for (int j = 0; j < RG; ++j) {
+            const int row = row0 + j * 16 + r;
+            bx[j] = (row < rows && kin) ? *reinterpret_cast<const float4*>(x + (long long)row * in_dim + k)
+                                        : make_float4(0.f, 0.f, 0.f, 0.f);
         }
-        s = wave_sum(s);
-        if (lane == 0) y[(long long)r * out_dim + o] = s + bias;
+#pragma unroll
+        for (int j = 0; j < RG; ++j) {
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, bx[j].x, acc[j], 0, 0, 0);
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, bx[j].y, acc[j], 0, 0, 0);
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, bx[j].z, acc[j], 0, 0, 0);
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, bx[j].w, acc[j], 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < RG; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) part[wave][j][lane][e] = acc[j][e];
+    __syncthreads();
+    // lane L of the tile holds D[o = 4*(L>>4) + e][row = L & 15]
+    for (int t = threadIdx.x; t < RG * 64 * 4; t += 512) {
+        const int j = t >> 8, L = (t >> 2) & 63, e = t & 3;
+        float v = part[0][j][L][e];
+#pragma unroll
+        for (int q = 1; q < 8; ++q) v += part[q][j][L][e];
+        const int o = o0 + 4 * (L >> 4) + e, row = row0 + j * 16 + (L & 15);
+        if (o < out_dim && row < rows) y[(long long)row * out_dim + o] = v + (b ? b[o] : 0.f);
     }
 }
 
@@ -161,7 +243,10 @@ int rr_global_pool(const void* x, int n, int c, int hw, int layout, int mode, fl
     if (layout == RR_NHWC) {
         if (c % 4) return fail(RR_EINVAL, "rr_global_pool: NHWC needs c % 4 == 0");
         dim3 grid((c + 255) / 256, n);
-        if (dtype == RR_BF16)
+        if (dtype == RR_BF16 && c % 8 == 0 && ((uintptr_t)x & 15) == 0)
+            hipLaunchKernelGGL(k_pool_nhwc_bf16x8, dim3((c + 511) / 512, n), dim3(1024), 0, s, (const uint4*)x, c, hw,
+                               mode, p, ip, eps, out);
+        else if (dtype == RR_BF16)
             hipLaunchKernelGGL(k_pool_nhwc<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, c, hw, mode, p, ip, eps, out);
         else if (dtype == RR_F32)
             hipLaunchKernelGGL(k_pool_nhwc<float>, grid, dim3(256), 0, s, (const float*)x, c, hw, mode, p, ip, eps, out);
@@ -191,10 +276,10 @@ int rr_l2n_rows(const float* x, int rows, int dim, float eps, float* y, void* st
 int rr_linear_rows(const float* x, int rows, int in_dim, const float* w, const float* b, int out_dim, float* y,
                    void* stream) {
     if (rows <= 0 || out_dim <= 0) return fail(RR_EINVAL, "rr_linear_rows: empty");
-    if (in_dim % 4 || in_dim <= 0 || in_dim > 64 * 4 * LIN_MAXV)
-        return fail(RR_EINVAL, "rr_linear_rows: in_dim must be a multiple of 4, <= 4096");
-    hipLaunchKernelGGL(k_linear_rows, dim3((out_dim + 3) / 4), dim3(256), 0, as_stream(stream), x, rows, in_dim, w, b,
-                       out_dim, y);
+    if (in_dim % 4 || in_dim <= 0) return fail(RR_EINVAL, "rr_linear_rows: in_dim must be a positive multiple of 4");
+    if ((((uintptr_t)x) | ((uintptr_t)w)) & 15) return fail(RR_EINVAL, "rr_linear_rows: x and w must be 16-byte aligned");
+    hipLaunchKernelGGL(k_linear_mfma, dim3((out_dim + 15) / 16, (rows + 63) / 64), dim3(512), 0, as_stream(stream), x,
+                       rows, in_dim, w, b, out_dim, y);
     return check_launch("rr_linear_rows");
 }
 

@@ -174,9 +174,13 @@ int rr_topk_merge(const double* in_scores, const long long* in_idx, int r, int n
  *   RR_TUNE_GEMM_ASTAT   0/1 allow the A-stationary tiles in the automatic choice
  *   RR_TUNE_GEMM_XCD_MAP 0/1 XCD-contiguous tile order (default 0)
  *   RR_TUNE_STREAM_1X1   0/1 weight-stationary streaming kernel for the
- *                        HBM-bound bf16 1x1 convs (default 1) */
+ *                        HBM-bound bf16 1x1 convs (default 1)
+ *   RR_TUNE_CONV3X3      0 off, 1 auto (default): direct 3x3 kernel with LDS
+ *                        halo patches for the bf16 stride-1 3x3 convs;
+ *                        2 / 3 prefer its 8x32 / 4x32 pixel tiles */
 enum rr_tune_key { RR_TUNE_GEMM_CONFIG = 0, RR_TUNE_GEMM_STAGES = 1, RR_TUNE_GEMM_WIDE = 2,
-                   RR_TUNE_GEMM_ASTAT = 3, RR_TUNE_GEMM_XCD_MAP = 4, RR_TUNE_STREAM_1X1 = 5 };
+                   RR_TUNE_GEMM_ASTAT = 3, RR_TUNE_GEMM_XCD_MAP = 4, RR_TUNE_STREAM_1X1 = 5,
+                   RR_TUNE_CONV3X3 = 6 };
 int rr_set_tuning(int key, int value);
 
 /* ----------------------------------------------------------- data helpers */

@@ -87,6 +87,29 @@ def test_conv_stream1x1(cuda, case, mode):
         E.lib().rr_set_tuning(5, 1)
 
 
+CONV3_CASES = [
+    # bf16 stride-1 3x3 shapes the direct LDS-patch kernel (rr_conv3.hip) takes
+    (2, 64, 16, 64, 64, 3, 1, 1, False, True),     # c_in = c_out = 64: weights resident in LDS
+    (2, 64, 8, 32, 128, 3, 1, 1, False, False),    # one input chunk, weight ring
+    (1, 128, 16, 64, 128, 3, 1, 1, False, True),   # two chunks
+    (1, 256, 8, 32, 256, 3, 1, 1, False, True),    # two channel tiles
+    (1, 512, 12, 32, 512, 3, 1, 1, False, True),   # 8 chunks, height only 4-divisible
+]
+
+
+@pytest.mark.parametrize("case", CONV3_CASES)
+@pytest.mark.parametrize("mode", [1, 2, 3, 0])
+def test_conv3x3_direct(cuda, case, mode):
+    """Direct 3x3 kernel (modes 1-3: auto / 8x32 / 4x32 tiles) and the
+    implicit-GEMM fallback (mode 0) against the float64 reference."""
+    from cirtorch import _engine as E
+    E.check(E.lib().rr_set_tuning(6, mode), "rr_set_tuning")
+    try:
+        _check_conv(cuda, case, "bf16", True)
+    finally:
+        E.lib().rr_set_tuning(6, 1)
+
+
 def _check_conv(cuda, case, prec, perm):
     n, cin, h, w, cout, k, s, p, use_res, leaky = case
     g = torch.Generator().manual_seed(hash(case) & 0xFFFF)

@@ -24,10 +24,15 @@ def main():
     ap.add_argument("--width", type=int, default=1024)
     ap.add_argument("--precision", default="bf16")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--tune", default="", help="rr_set_tuning pairs key=value[,key=value]")
     args = ap.parse_args()
     from cirtorch import _ops
     from cirtorch.backbones import resnet
     from cirtorch.models.init import random_init_
+    from cirtorch import _engine as E
+    for kv in filter(None, args.tune.split(",")):
+        k_, v_ = kv.split("=")
+        E.check(E.lib().rr_set_tuning(int(k_), int(v_)), "rr_set_tuning")
 
     body = resnet.__dict__[args.arch](precision=args.precision)
     random_init_(body, 0)
