@@ -279,6 +279,16 @@ def main():
                                 "frac": flops / tk / 1e12 / peak, "traffic": None,
                                 "note": "per-rank screening GEMM FLOPs 2*Q*n_local*D / whole search time"}}
 
+    traffic, traffic_note = None, "no PMC traffic file for this config"
+    tpath = os.path.join(REPO, "profiles", "r01_pmc_traffic.json")
+    if os.path.exists(tpath):
+        t = json.load(open(tpath))
+        c = t.get("config", {})
+        if (c.get("arch"), c.get("precision"), c.get("image")) == (args.arch, args.precision, [3, H, W]):
+            traffic = t["hbm_bytes_per_image"] * B
+            traffic_note = ("HBM bytes of the step's extractor dispatches from rocprofv3 PMC (2 x FETCH_SIZE + "
+                            "WRITE_SIZE, profiles/r01_pmc_traffic.json, %d-image forwards, commit %s)"
+                            % (c.get("batch", 0), c.get("source_commit", "?")))
     fl_img = conv_flops_per_image(net.body, H, W)
     costs = layer_costs(net.body, H, W, 2 if args.precision == "bf16" else 4)
     peak_m = (PEAK_BF16_TFLOPS if args.precision == "bf16" else PEAK_F32_TFLOPS) * 1e12
@@ -308,8 +318,11 @@ def main():
                    "dim": args.dim,
                    "k": args.k, "parallelism": "dp%d (images) x db-shard%d" % (world, world)},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                     "frac": achieved / peak, "traffic": None,
-                     "note": "dominant kernel = k_conv (implicit-GEMM MFMA conv family, 53 launches/forward); "
+                     "frac": achieved / peak, "traffic": traffic, "traffic_note": traffic_note,
+                     "algorithmic_bytes": bytes_img * B,
+                     "note": "dominant kernel family = the extractor body's 53 conv launches per forward (k_stem_pool, "
+                             "k_conv3x3, k_stream1x1, k_igemm; their per-kernel rocprof averages sum to this time, "
+                             "see profiles/); "
                              "%.2f GFLOP/img x %d img / extract-body event time %.3f ms" % (fl_img / 1e9, B, body_ms)},
         "roofline_layers": {"floor_ms": floor_ms, "measured_ms": body_ms, "frac": floor_ms / body_ms,
                             "hbm_bytes_per_img": bytes_img, "peak_mfma_tflops": peak_m / 1e12,
