@@ -218,15 +218,33 @@ class ResNet(nn.Module):
             t = _ops.maxpool2d(t, 3, 2, 1)
         outs = OrderedDict()
         outs["mod1"] = t
-        for mod_id, blocks in enumerate(plan["mods"]):
-            for steps, proj in blocks:
-                res = self._conv(t, proj) if proj is not None else t
-                y = t
-                for st in steps[:-1]:
-                    y = self._conv(y, st)
+        flat = [(mod_id, steps, proj) for mod_id, blocks in enumerate(plan["mods"]) for steps, proj in blocks]
+        pending = None  # conv1 output of the next block, produced by a fused boundary launch
+        for i, (mod_id, steps, proj) in enumerate(flat):
+            res = self._conv(t, proj) if proj is not None else t
+            y = t
+            for j, st in enumerate(steps[:-1]):
+                y = pending if (j == 0 and pending is not None) else self._conv(y, st)
+            pending = None
+            nxt = flat[i + 1][1][0] if i + 1 < len(flat) else None
+            if self._pairable(steps[-1], nxt):
+                last = steps[-1]
+                t, pending = _ops.conv1x1_pair(y, last.w, last.scale, last.shift, res, last.leaky, last.slope,
+                                               nxt.w, nxt.scale, nxt.shift, nxt.c_out, nxt.leaky, nxt.slope)
+            else:
                 t = self._conv(y, steps[-1], residual=res)
-            outs["mod%d" % (mod_id + 2)] = t
+            if i + 1 == len(flat) or flat[i + 1][0] != mod_id:
+                outs["mod%d" % (mod_id + 2)] = t
         return OrderedDict((k, v.permute(0, 3, 1, 2)) for k, v in outs.items())
+
+    def _pairable(self, last, nxt):
+        """conv3 of a 64->256 bottleneck followed by a stride-1 1x1 conv1 (256 -> 64/128):
+        one fused rr_conv1x1_pair launch (bf16)."""
+        if nxt is None or self.engine_dtype != torch.bfloat16 or os.environ.get("RR_PAIR_FUSED", "1") == "0":
+            return False
+        return (last.kh == 1 and last.stride == 1 and last.perm and last.c_out == 256 and last.w.shape[1] == 64
+                and nxt.kh == 1 and nxt.stride == 1 and nxt.pad == 0 and nxt.perm and nxt.w.shape[1] == 256
+                and nxt.c_out in (64, 128))
 
 
 _NETS = {

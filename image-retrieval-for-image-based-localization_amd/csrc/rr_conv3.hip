@@ -313,7 +313,8 @@ void launch_c3(const ConvArgs& a, hipStream_t s) {
 
 }  // namespace
 
-int g_conv3_mode = 1;  // rr_set_tuning(RR_TUNE_CONV3X3): 0 off, 1 auto, 2 / 3 prefer 8x32 / 4x32 tiles
+int g_conv3_mode = 1;  // rr_set_tuning(RR_TUNE_CONV3X3): 0 off, 1 auto, 2 / 3 prefer 8x32 / 4x32 tiles,
+                       // 4 / 6 A-stationary with 1x8 / 1x4 waves (auto: 2x4)
 
 // bf16 3x3 / stride 1 / pad 1 with PERM32 weights, bf16 out, no residual, and
 // image sizes the tiles divide; returns false otherwise (caller falls back to
@@ -333,7 +334,10 @@ bool launch_conv3x3(const ConvArgs& a, hipStream_t s) {
         g_c3_cus = cus;
     }
     if (a.cin == 64 && a.cout == 64 && a.h % 8 == 0) {
-        launch_c3<64, 8, 32, 1, 4, true>(a, s);
+        // 8 waves (2 per SIMD) measured fastest: 125 us vs 146 (4 waves) at 32 x 192x256x64
+        if (g_conv3_mode == 4) launch_c3<64, 8, 32, 1, 8, true>(a, s);
+        else if (g_conv3_mode == 6) launch_c3<64, 8, 32, 1, 4, true>(a, s);
+        else launch_c3<64, 8, 32, 2, 4, true>(a, s);
         return true;
     }
     if (a.cout % 128 == 0 && a.cout <= 512) {

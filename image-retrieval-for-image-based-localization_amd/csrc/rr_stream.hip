@@ -209,6 +209,173 @@ __global__ void __launch_bounds__(64 * NW) k_stream1x1(ConvArgs a, int nslices) 
     }
 }
 
+// ---------------------------------------------------------------------------
+// Fused bottleneck boundary (bf16, the 64/256-channel stage of ResNet-50/101/
+// 152): block i's conv3 (1x1, 64 -> 256, BN, + residual, activation) and block
+// i+1's conv1 (1x1, 256 -> C1, BN, activation) in one pass.
+//   y = act3(W3 . x * s3 + h3 + r)   is stored once and, still in registers,
+//   z = act1(W1 . y * s1 + h1)       consumes it as the second GEMM's B operand:
+// with PERM32 rows a lane's accumulator pair holds 8 consecutive y channels of
+// one pixel, which is exactly an MFMA B fragment (k = channel), so y is never
+// re-read from HBM (-2 B x 256 per pixel vs two launches).  Both weight slices
+// (32 KiB + C1 x 512 B) and the affines stay in LDS; activations stream
+// HBM -> VGPR D strips deep as in k_stream1x1.
+struct PairArgs {
+    const bf16_t* x;   // [P][64]
+    const bf16_t* w3;  // [256][64]  PERM32 rows
+    const float *s3, *h3;
+    const bf16_t* res; // [P][256]
+    const bf16_t* w1;  // [C1][256]  PERM32 rows
+    const float *s1, *h1;
+    bf16_t* y;         // [P][256]
+    bf16_t* z;         // [P][C1]
+    long long P;
+    int act3, act1;
+    float slope3, slope1;
+};
+
+template <int C1, int D>
+__global__ void __launch_bounds__(512) k_stream_pair(PairArgs a) {
+    constexpr int K3 = 64, C3 = 256, NW = 8;
+    constexpr int NK3 = K3 / 32, NR3 = C3 / 32, NF1 = C1 / 16, NK1 = C3 / 32;
+    __shared__ __attribute__((aligned(16))) char sW3[C3 * K3 * 2];
+    __shared__ __attribute__((aligned(16))) char sW1[C1 * C3 * 2];
+    __shared__ __attribute__((aligned(16))) float sS3[C3], sH3[C3], sS1[C1], sH1[C1];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    for (int i = tid; i < C3 * K3 / 8; i += 64 * NW) {
+        const int r = i / (K3 / 8), c = i - r * (K3 / 8);
+        *reinterpret_cast<uint4*>(sW3 + wswz<K3>(r, c)) = reinterpret_cast<const uint4*>(a.w3)[i];
+    }
+    for (int i = tid; i < C1 * C3 / 8; i += 64 * NW) {
+        const int r = i / (C3 / 8), c = i - r * (C3 / 8);
+        *reinterpret_cast<uint4*>(sW1 + wswz<C3>(r, c)) = reinterpret_cast<const uint4*>(a.w1)[i];
+    }
+    for (int i = tid; i < C3; i += 64 * NW) {
+        sS3[i] = a.s3[i];
+        sH3[i] = a.h3[i];
+    }
+    for (int i = tid; i < C1; i += 64 * NW) {
+        sS1[i] = a.s1[i];
+        sH1[i] = a.h1[i];
+    }
+    __syncthreads();
+
+    const int r16 = lane & 15, kq = lane >> 4;
+    const long long P = a.P;
+    const int nstrips = (int)((P + 15) / 16);
+    const int gw = (int)blockIdx.x * NW + wave, GW = (int)gridDim.x * NW;
+    const int nmine = gw < nstrips ? (nstrips - gw + GW - 1) / GW : 0;
+    if (nmine == 0) return;
+    const int niter = (nmine + D - 1) / D * D;
+    const bool leaky3 = a.act3 == RR_ACT_LEAKY, leaky1 = a.act1 == RR_ACT_LEAKY;
+    auto strip_of = [&](int i) { return gw + (i < nmine ? i : nmine - 1) * GW; };
+    auto pix = [&](int s) {
+        const long long p = (long long)s * 16 + r16;
+        return p < P ? p : P - 1;
+    };
+
+    uint4 bq[D][NK3], rq[D][NR3];
+    auto load = [&](int d, int s) {
+        const long long p = pix(s);
+        const bf16_t* xs = a.x + p * K3 + 8 * kq;
+#pragma unroll
+        for (int kk = 0; kk < NK3; ++kk) bq[d][kk] = *reinterpret_cast<const uint4*>(xs + kk * 32);
+        const bf16_t* rs = a.res + p * C3 + 8 * kq;
+#pragma unroll
+        for (int i2 = 0; i2 < NR3; ++i2) rq[d][i2] = *reinterpret_cast<const uint4*>(rs + 32 * i2);
+    };
+#pragma unroll
+    for (int d = 0; d < D; ++d) load(d, strip_of(d));
+
+    for (int it = 0; it < niter; it += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const int i = it + d;
+            const long long p = (long long)strip_of(i) * 16 + r16;
+            const bool st = i < nmine && p < P;
+            uint4 yq[NR3];
+            // ---- y = act3(W3 x * s3 + h3 + r): one 32-channel pair at a time
+#pragma unroll
+            for (int i2 = 0; i2 < NR3; ++i2) {
+                int abase = 0;
+                asm volatile("" : "+v"(abase));  // keep the weight fragments in LDS (no hoisting into VGPRs)
+                sf32x4_t acc[2] = {(sf32x4_t){0.f, 0.f, 0.f, 0.f}, (sf32x4_t){0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+                for (int kk = 0; kk < NK3; ++kk)
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const uint4 av = *reinterpret_cast<const uint4*>(sW3 + abase + wswz<K3>((2 * i2 + h) * 16 + r16, kk * 4 + kq));
+                        acc[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(sbf16x8_t, av),
+                                                                         __builtin_bit_cast(sbf16x8_t, bq[d][kk]),
+                                                                         acc[h], 0, 0, 0);
+                    }
+                const int c = 32 * i2 + 8 * kq;
+                const uint4 q = rq[d][i2];
+                const unsigned w4[4] = {q.x, q.y, q.z, q.w};
+                float v[8];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    v[r] = acc[0][r] * sS3[c + r] + sH3[c + r];
+                    v[4 + r] = acc[1][r] * sS3[c + 4 + r] + sH3[c + 4 + r];
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    v[2 * r] += __uint_as_float(w4[r] << 16);
+                    v[2 * r + 1] += __uint_as_float(w4[r] & 0xffff0000u);
+                }
+                if (leaky3) {
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * a.slope3;
+                }
+                yq[i2].x = pack_bf16x2(v[0], v[1]);
+                yq[i2].y = pack_bf16x2(v[2], v[3]);
+                yq[i2].z = pack_bf16x2(v[4], v[5]);
+                yq[i2].w = pack_bf16x2(v[6], v[7]);
+                if (st) *reinterpret_cast<uint4*>(a.y + p * C3 + c) = yq[i2];
+            }
+            load(d, strip_of(i + D));  // refill this slot: strip i + D
+            // ---- z = act1(W1 y * s1 + h1), y straight from registers
+            sf32x4_t zacc[NF1];
+#pragma unroll
+            for (int o = 0; o < NF1; ++o) zacc[o] = (sf32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kk = 0; kk < NK1; ++kk) {
+                int abase = 0;
+                asm volatile("" : "+v"(abase));
+#pragma unroll
+                for (int o = 0; o < NF1; ++o) {
+                    const uint4 av = *reinterpret_cast<const uint4*>(sW1 + abase + wswz<C3>(o * 16 + r16, kk * 4 + kq));
+                    zacc[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(sbf16x8_t, av),
+                                                                      __builtin_bit_cast(sbf16x8_t, yq[kk]), zacc[o],
+                                                                      0, 0, 0);
+                }
+            }
+#pragma unroll
+            for (int o2 = 0; o2 < NF1 / 2; ++o2) {
+                const int c = 32 * o2 + 8 * kq;
+                float v[8];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    v[r] = zacc[2 * o2][r] * sS1[c + r] + sH1[c + r];
+                    v[4 + r] = zacc[2 * o2 + 1][r] * sS1[c + 4 + r] + sH1[c + 4 + r];
+                }
+                if (leaky1) {
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * a.slope1;
+                }
+                uint4 o;
+                o.x = pack_bf16x2(v[0], v[1]);
+                o.y = pack_bf16x2(v[2], v[3]);
+                o.z = pack_bf16x2(v[4], v[5]);
+                o.w = pack_bf16x2(v[6], v[7]);
+                if (st) *reinterpret_cast<uint4*>(a.z + p * C1 + c) = o;
+            }
+        }
+    }
+}
+
 int g_stream_cus = 0;
 
 template <int TC, int K, int FN, int D, int NW>
@@ -258,4 +425,44 @@ bool launch_stream1x1(const ConvArgs& a, hipStream_t s) {
     return false;
 }
 
+int g_pair_cus = 0;
+
 }  // namespace rr
+
+using namespace rr;
+
+extern "C" int rr_conv1x1_pair(const void* x, long long p, int c_in, const void* w3, const float* scale3,
+                               const float* shift3, int c_mid, const void* residual, int act3, float slope3,
+                               const void* w1, const float* scale1, const float* shift1, int c_out, int act1,
+                               float slope1, void* y, void* z, int dtype, void* stream) {
+    if (dtype != RR_BF16) return fail(RR_EINVAL, "rr_conv1x1_pair: bf16 only");
+    if (c_in != 64 || c_mid != 256 || (c_out != 64 && c_out != 128))
+        return fail(RR_EINVAL, "rr_conv1x1_pair: shapes (c_in 64, c_mid 256, c_out 64|128) only");
+    if (!x || !w3 || !scale3 || !shift3 || !residual || !w1 || !scale1 || !shift1 || !y || !z)
+        return fail(RR_EINVAL, "rr_conv1x1_pair: null pointer");
+    if (p <= 0) return fail(RR_EINVAL, "rr_conv1x1_pair: empty");
+    if ((((uintptr_t)x) | ((uintptr_t)residual) | ((uintptr_t)y) | ((uintptr_t)z) | ((uintptr_t)w3) |
+         ((uintptr_t)w1)) & 15)
+        return fail(RR_EINVAL, "rr_conv1x1_pair: 16-byte alignment required");
+    if (act3 != RR_ACT_IDENTITY && act3 != RR_ACT_LEAKY) return fail(RR_EINVAL, "rr_conv1x1_pair: act3");
+    if (act1 != RR_ACT_IDENTITY && act1 != RR_ACT_LEAKY) return fail(RR_EINVAL, "rr_conv1x1_pair: act1");
+    if (g_pair_cus == 0) {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 256;
+        g_pair_cus = cus;
+    }
+    PairArgs a;
+    a.x = (const bf16_t*)x; a.w3 = (const bf16_t*)w3; a.s3 = scale3; a.h3 = shift3; a.res = (const bf16_t*)residual;
+    a.w1 = (const bf16_t*)w1; a.s1 = scale1; a.h1 = shift1; a.y = (bf16_t*)y; a.z = (bf16_t*)z; a.P = p;
+    a.act3 = act3; a.act1 = act1; a.slope3 = slope3; a.slope1 = slope1;
+    const long long nstrips = (p + 15) / 16;
+    long long grid = (nstrips + 7) / 8;
+    if (grid > g_pair_cus) grid = g_pair_cus;
+    if (c_out == 64)
+        hipLaunchKernelGGL((k_stream_pair<64, 2>), dim3((unsigned)grid), dim3(512), 0, as_stream(stream), a);
+    else
+        hipLaunchKernelGGL((k_stream_pair<128, 2>), dim3((unsigned)grid), dim3(512), 0, as_stream(stream), a);
+    return check_launch("rr_conv1x1_pair");
+}

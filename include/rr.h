@@ -91,6 +91,19 @@ int rr_conv2d_fused(const void* x, const void* w, const float* scale, const floa
 int rr_pack_conv_weights(const float* w, int c_out, int c_in, int kh, int kw, int c_in_pad,
                          int k_packed, int perm32, void* out, int dtype, void* stream);
 
+/* Fused bottleneck boundary, bf16, PERM32-packed weights (1x1 convs):
+ *   y = act3(conv1x1(x, w3) * scale3 + shift3 + residual)      [p][c_mid]
+ *   z = act1(conv1x1(y, w1) * scale1 + shift1)                 [p][c_out]
+ * i.e. conv3 + bn3 + residual add + activation of ResidualBlock i and conv1 +
+ * bn1 + activation of block i + 1 (cirtorch/backbones/misc.py:166-203), in one
+ * pass that never re-reads y.  p = pixels (n*h*w, stride 1).  Shapes: c_in 64,
+ * c_mid 256, c_out 64 or 128 (the 256-channel stage); anything else returns
+ * RR_EINVAL and the caller runs the two rr_conv2d_fused launches instead. */
+int rr_conv1x1_pair(const void* x, long long p, int c_in, const void* w3, const float* scale3,
+                    const float* shift3, int c_mid, const void* residual, int act3, float slope3,
+                    const void* w1, const float* scale1, const float* shift1, int c_out, int act1,
+                    float slope1, void* y, void* z, int dtype, void* stream);
+
 /* 3x3/s2/p1 style max pooling, NHWC.  Replaces nn.MaxPool2d(3, stride=2,
  * padding=1) of the stem (cirtorch/backbones/resnet.py:65). */
 int rr_maxpool2d(const void* x, int n, int h, int w, int c, int k, int stride, int pad,
@@ -177,7 +190,8 @@ int rr_topk_merge(const double* in_scores, const long long* in_idx, int r, int n
  *                        HBM-bound bf16 1x1 convs (default 1)
  *   RR_TUNE_CONV3X3      0 off, 1 auto (default): direct 3x3 kernel with LDS
  *                        halo patches for the bf16 stride-1 3x3 convs;
- *                        2 / 3 prefer its 8x32 / 4x32 pixel tiles */
+ *                        2 / 3 prefer its 8x32 / 4x32 pixel tiles, 4 / 6 use
+ *                        1x8 / 1x4 waves for the c_in = 64 A-stationary form */
 enum rr_tune_key { RR_TUNE_GEMM_CONFIG = 0, RR_TUNE_GEMM_STAGES = 1, RR_TUNE_GEMM_WIDE = 2,
                    RR_TUNE_GEMM_ASTAT = 3, RR_TUNE_GEMM_XCD_MAP = 4, RR_TUNE_STREAM_1X1 = 5,
                    RR_TUNE_CONV3X3 = 6 };

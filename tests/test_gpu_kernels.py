@@ -98,9 +98,9 @@ CONV3_CASES = [
 
 
 @pytest.mark.parametrize("case", CONV3_CASES)
-@pytest.mark.parametrize("mode", [1, 2, 3, 0])
+@pytest.mark.parametrize("mode", [1, 2, 3, 4, 6, 0])
 def test_conv3x3_direct(cuda, case, mode):
-    """Direct 3x3 kernel (modes 1-3: auto / 8x32 / 4x32 tiles) and the
+    """Direct 3x3 kernel (modes 1-4, 6: auto / 8x32 / 4x32 tiles / A-stationary wave layouts) and the
     implicit-GEMM fallback (mode 0) against the float64 reference."""
     from cirtorch import _engine as E
     E.check(E.lib().rr_set_tuning(6, mode), "rr_set_tuning")
@@ -258,3 +258,43 @@ def test_stem_conv_pool(cuda, shape, norm):
     assert (got - un).abs().max().item() <= 8e-3 * ref.abs().max().item()
     # most values are bit-identical (only fp32 summation order differs)
     assert (got == un).float().mean().item() > 0.95
+
+
+@pytest.mark.parametrize("c_out", [64, 128])
+@pytest.mark.parametrize("shape", [(2, 23, 37), (1, 64, 96)])
+def test_conv1x1_pair(cuda, c_out, shape):
+    """Fused bottleneck boundary (rr_conv1x1_pair): conv3 (64->256) + BN +
+    residual + leaky of block i and conv1 (256->c_out) + BN + leaky of block
+    i+1 (cirtorch/backbones/misc.py:166-203) vs a float64 restatement, and vs
+    the two separate engine launches (same bf16 roundings, so bit-identical
+    up to fp32 summation order)."""
+    n, h, w = shape
+    g = torch.Generator().manual_seed(c_out * 7 + h)
+    ops = _ops()
+    x = _bf16_round(torch.randn(n, 64, h, w, generator=g))
+    w3 = _bf16_round(torch.randn(256, 64, 1, 1, generator=g) * (2.0 / 64) ** 0.5)
+    w1 = _bf16_round(torch.randn(c_out, 256, 1, 1, generator=g) * (2.0 / 256) ** 0.5)
+    s3, h3 = torch.rand(256, generator=g) + 0.5, torch.randn(256, generator=g) * 0.1
+    s1, h1 = torch.rand(c_out, generator=g) + 0.5, torch.randn(c_out, generator=g) * 0.1
+    res = _bf16_round(torch.randn(n, 256, h, w, generator=g))
+    yr = F.leaky_relu(F.conv2d(x.double(), w3.double()) * s3.double()[None, :, None, None]
+                      + h3.double()[None, :, None, None] + res.double(), 0.01)
+    yb = _bf16_round(yr.float()).double()
+    zr = F.leaky_relu(F.conv2d(yb, w1.double()) * s1.double()[None, :, None, None] + h1.double()[None, :, None, None],
+                      0.01)
+    bf = torch.bfloat16
+    xe = x.permute(0, 2, 3, 1).contiguous().to(bf).to(cuda)
+    re = res.permute(0, 2, 3, 1).contiguous().to(bf).to(cuda)
+    w3p = ops.pack_conv_weights(w3.to(cuda), 64, bf, perm32=True)
+    w1p = ops.pack_conv_weights(w1.to(cuda), 256, bf, perm32=True)
+    c = [t.to(cuda) for t in (s3, h3, s1, h1)]
+    y, z = ops.conv1x1_pair(xe, w3p, c[0], c[1], re, True, 0.01, w1p, c[2], c[3], c_out, True, 0.01)
+    gy = y.float().permute(0, 3, 1, 2).cpu().double()
+    gz = z.float().permute(0, 3, 1, 2).cpu().double()
+    assert (gy - yr).abs().max().item() <= 8e-3 * yr.abs().max().item()
+    assert (gz - zr).abs().max().item() <= 1.6e-2 * zr.abs().max().item()
+    # the unfused engine path on the same inputs
+    y2 = ops.conv2d_fused(xe, w3p, 1, 1, 1, 0, 256, c[0], c[1], residual=re, leaky=True, perm32=True)
+    z2 = ops.conv2d_fused(y2, w1p, 1, 1, 1, 0, c_out, c[2], c[3], leaky=True, perm32=True)
+    assert torch.equal(y.cpu(), y2.cpu())
+    assert (z.float() == z2.float()).float().mean().item() > 0.99
