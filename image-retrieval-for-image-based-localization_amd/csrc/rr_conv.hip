@@ -409,7 +409,12 @@ namespace rr {
 void set_gemm_tuning(int key, int value);
 }
 extern "C" int rr_set_tuning(int key, int value) {
-    if (key < 0 || key > 6) return fail(RR_EINVAL, "rr_set_tuning: unknown key");
+    if (key < 0 || key > 7) return fail(RR_EINVAL, "rr_set_tuning: unknown key");
+    if (key == RR_TUNE_GRID_CUS) {
+        if (value < 0) return fail(RR_EINVAL, "rr_set_tuning: RR_TUNE_GRID_CUS must be >= 0");
+        rr::g_grid_cap = value;
+        return RR_OK;
+    }
     if (key == RR_TUNE_STREAM_1X1) rr::g_stream_mode = value;
     else if (key == RR_TUNE_CONV3X3) rr::g_conv3_mode = value;
     else rr::set_gemm_tuning(key, value);

@@ -300,13 +300,12 @@ __global__ void __launch_bounds__(64 * WC * WP) k_conv3x3(ConvArgs a, int tiles_
     }
 }
 
-int g_c3_cus = 0;
-
 template <int TC, int TH, int TW, int WC, int WP, bool ARES>
 void launch_c3(const ConvArgs& a, hipStream_t s) {
     const int tiles_w = a.w_ / TW, tiles_h = a.h / TH, tiles_c = a.cout / TC;
     const long long ntl = (long long)a.n * tiles_h * tiles_w * tiles_c;
-    const int grid = (int)(ntl < g_c3_cus ? ntl : g_c3_cus);
+    const int cus = grid_cus();
+    const int grid = (int)(ntl < cus ? ntl : cus);
     hipLaunchKernelGGL((k_conv3x3<TC, TH, TW, WC, WP, ARES>), dim3(grid), dim3(64 * WC * WP), 0, s, a, tiles_w,
                        tiles_w * tiles_h, tiles_c, (int)ntl);
 }
@@ -326,13 +325,7 @@ bool launch_conv3x3(const ConvArgs& a, hipStream_t s) {
     if (a.cin % 64 || a.kp != 9 * a.cin || a.w_ % 32) return false;
     if ((long long)a.n * a.h * a.w_ * a.cin * 2 >= (1ll << 31)) return false;
     if ((long long)a.n * a.h * a.w_ >= (1ll << 31) / 2) return false;
-    if (g_c3_cus == 0) {
-        int dev = 0, cus = 256;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            cus = 256;
-        g_c3_cus = cus;
-    }
+    const int g_c3_cus = grid_cus();
     if (a.cin == 64 && a.cout == 64 && a.h % 8 == 0) {
         // 8 waves (2 per SIMD) measured fastest: 125 us vs 146 (4 waves) at 32 x 192x256x64
         if (g_conv3_mode == 4) launch_c3<64, 8, 32, 1, 8, true>(a, s);

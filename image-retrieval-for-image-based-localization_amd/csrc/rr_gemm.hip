@@ -483,26 +483,21 @@ __global__ void __launch_bounds__(64 * WC * WP, ((NS == 2 && AK * TC <= 256) || 
     }
 }
 
-static int g_num_cus = 0;
 static int g_stages = 0;
 static bool g_wide = true;
 static bool g_ast = false;
 static bool g_xmap = false;
+static bool g_env_done = false;
 
 static int num_cus() {
-    if (g_num_cus == 0) {
-        int dev = 0, cus = 256;
-        if (hipGetDevice(&dev) == hipSuccess &&
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
-            g_num_cus = cus;
-        else
-            g_num_cus = 256;
+    if (!g_env_done) {
         const char* e = getenv("RR_GEMM_STAGES");
         g_stages = (e && (e[0] == '3')) ? 3 : 2;
         const char* w = getenv("RR_GEMM_WIDE");
         g_wide = !(w && w[0] == '0');
+        g_env_done = true;
     }
-    return g_num_cus;
+    return grid_cus();
 }
 
 template <typename T, typename TO, int TC, int TP, int WC, int WP, int NS, int AK = 0>

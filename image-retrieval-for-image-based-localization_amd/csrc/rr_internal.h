@@ -15,6 +15,12 @@ int fail(int code, const std::string& msg);
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// CUs one persistent launch may spread over: the device's CU count, capped by
+// rr_set_tuning(RR_TUNE_GRID_CUS, n) (0 = no cap) so that launches on two
+// streams can share the chip (rr_runtime.hip).
+int grid_cus();
+extern int g_grid_cap;
+
 // Launch-error check: every entry point ends with this.
 inline int check_launch(const char* what) {
     hipError_t e = hipGetLastError();

@@ -9,6 +9,20 @@ namespace rr {
 
 static thread_local std::string g_err;
 
+int g_grid_cap = 0;
+static int g_dev_cus = 0;
+
+int grid_cus() {
+    if (g_dev_cus == 0) {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 256;
+        g_dev_cus = cus;
+    }
+    return (g_grid_cap > 0 && g_grid_cap < g_dev_cus) ? g_grid_cap : g_dev_cus;
+}
+
 void set_error(const std::string& msg) { g_err = msg; }
 int fail(int code, const std::string& msg) {
     g_err = msg;

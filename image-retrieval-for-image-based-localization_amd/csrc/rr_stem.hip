@@ -225,7 +225,6 @@ __global__ void k_stem_pack(const float* __restrict__ w, bf16_t* __restrict__ ou
     out[i] = f2bf(v);
 }
 
-int g_stem_cus = 0;
 
 }  // namespace
 
@@ -270,13 +269,7 @@ extern "C" int rr_stem_conv_pool(const float* x, int n, int h, int w, const floa
     const int tiles_w = (wp + PW - 1) / PW, tiles_h = (hp + PH - 1) / PH;
     const long long ntiles = (long long)n * tiles_h * tiles_w;
     if (ntiles >= (1ll << 31)) return fail(RR_EINVAL, "rr_stem_conv_pool: too many tiles");
-    if (g_stem_cus == 0) {
-        int dev = 0, cus = 256;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            cus = 256;
-        g_stem_cus = cus;
-    }
+    const int g_stem_cus = grid_cus();
     const int grid = (int)(ntiles < g_stem_cus ? ntiles : g_stem_cus);
     hipLaunchKernelGGL((k_stem_pool<PH, PW>), dim3(grid), dim3(NT), 0, as_stream(stream), a, tiles_w,
                        tiles_w * tiles_h, (int)ntiles);

@@ -376,17 +376,10 @@ __global__ void __launch_bounds__(512) k_stream_pair(PairArgs a) {
     }
 }
 
-int g_stream_cus = 0;
 
 template <int TC, int K, int FN, int D, int NW>
 void launch_s(const ConvArgs& a, hipStream_t s) {
-    if (g_stream_cus == 0) {
-        int dev = 0, cus = 256;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            cus = 256;
-        g_stream_cus = cus;
-    }
+    const int g_stream_cus = grid_cus();
     constexpr int LDS = TC * K * 2 + TC * 8;
     constexpr int PER_CU = (160 * 1024 / LDS) >= 2 && NW <= 8 ? (NW <= 4 ? 4 : 2) : 1;
     const int nslices = a.cout / TC;
@@ -425,7 +418,6 @@ bool launch_stream1x1(const ConvArgs& a, hipStream_t s) {
     return false;
 }
 
-int g_pair_cus = 0;
 
 }  // namespace rr
 
@@ -446,13 +438,7 @@ extern "C" int rr_conv1x1_pair(const void* x, long long p, int c_in, const void*
         return fail(RR_EINVAL, "rr_conv1x1_pair: 16-byte alignment required");
     if (act3 != RR_ACT_IDENTITY && act3 != RR_ACT_LEAKY) return fail(RR_EINVAL, "rr_conv1x1_pair: act3");
     if (act1 != RR_ACT_IDENTITY && act1 != RR_ACT_LEAKY) return fail(RR_EINVAL, "rr_conv1x1_pair: act1");
-    if (g_pair_cus == 0) {
-        int dev = 0, cus = 256;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            cus = 256;
-        g_pair_cus = cus;
-    }
+    const int g_pair_cus = grid_cus();
     PairArgs a;
     a.x = (const bf16_t*)x; a.w3 = (const bf16_t*)w3; a.s3 = scale3; a.h3 = shift3; a.res = (const bf16_t*)residual;
     a.w1 = (const bf16_t*)w1; a.s1 = scale1; a.h1 = shift1; a.y = (bf16_t*)y; a.z = (bf16_t*)z; a.P = p;

@@ -191,10 +191,12 @@ int rr_topk_merge(const double* in_scores, const long long* in_idx, int r, int n
  *   RR_TUNE_CONV3X3      0 off, 1 auto (default): direct 3x3 kernel with LDS
  *                        halo patches for the bf16 stride-1 3x3 convs;
  *                        2 / 3 prefer its 8x32 / 4x32 pixel tiles, 4 / 6 use
- *                        1x8 / 1x4 waves for the c_in = 64 A-stationary form */
+ *                        1x8 / 1x4 waves for the c_in = 64 A-stationary form
+ *   RR_TUNE_GRID_CUS     cap on the CUs one persistent launch spreads over
+ *                        (0 = all; e.g. half the chip for two concurrent streams) */
 enum rr_tune_key { RR_TUNE_GEMM_CONFIG = 0, RR_TUNE_GEMM_STAGES = 1, RR_TUNE_GEMM_WIDE = 2,
                    RR_TUNE_GEMM_ASTAT = 3, RR_TUNE_GEMM_XCD_MAP = 4, RR_TUNE_STREAM_1X1 = 5,
-                   RR_TUNE_CONV3X3 = 6 };
+                   RR_TUNE_CONV3X3 = 6, RR_TUNE_GRID_CUS = 7 };
 int rr_set_tuning(int key, int value);
 
 /* ----------------------------------------------------------- data helpers */

@@ -79,6 +79,15 @@ int main() {
     run("line: read 201 MB + write 805 MB", [&] { hipLaunchKernelGGL(k_line, dim3(blocks), dim3(256), 0, 0, (const uint4*)in, (uint4*)out, nin, nout); }, (double)(in_b + out_b));
     run("line: copy 805 MB (read=write)", [&] { hipLaunchKernelGGL(k_line, dim3(blocks), dim3(256), 0, 0, (const uint4*)out, (uint4*)in, nout / 4, nout / 4); }, (double)(in_b * 2));
     run("frag: read 201 MB + write 805 MB", [&] { hipLaunchKernelGGL(k_frag, dim3(blocks), dim3(256), 0, 0, (const uint4*)in, (uint4*)out, rows, wmul); }, (double)(in_b + out_b));
+    for (int nb : {64, 128, 256}) {
+        for (int thr : {256, 1024}) {
+            char nm[96];
+            snprintf(nm, sizeof nm, "line: read 201+write 805, %d blocks x %d", nb, thr);
+            run(nm, [&] { hipLaunchKernelGGL(k_line, dim3(nb), dim3(thr), 0, 0, (const uint4*)in, (uint4*)out, nin, nout); }, (double)(in_b + out_b));
+            snprintf(nm, sizeof nm, "line: read only 805, %d blocks x %d", nb, thr);
+            run(nm, [&] { hipLaunchKernelGGL(k_line, dim3(nb), dim3(thr), 0, 0, (const uint4*)out, (uint4*)in, nout, 0ll); }, (double)out_b);
+        }
+    }
     run("frag: read 201 MB + write 201 MB", [&] { hipLaunchKernelGGL(k_frag, dim3(blocks), dim3(256), 0, 0, (const uint4*)in, (uint4*)out, rows, 1); }, (double)(2 * in_b));
     return 0;
 }
