@@ -71,18 +71,29 @@ def conv2d_fused(x, w_packed, kh, kw, stride, pad, c_out, scale=None, shift=None
     return y
 
 
-def conv1x1_pair(x, w3, scale3, shift3, residual, leaky3, slope3, w1, scale1, shift1, c_out, leaky1, slope1):
-    """Fused y = act3(conv1x1(x, w3)*scale3 + shift3 + residual); z = act1(conv1x1(y, w1)*scale1 + shift1)
+def conv1x1_pair(x, w3, scale3, shift3, residual, leaky3, slope3, w1, scale1, shift1, c_out, leaky1, slope1,
+                 proj=None):
+    """Fused y = act3(conv1x1(x, w3)*scale3 + shift3 + shortcut); z = act1(conv1x1(y, w1)*scale1 + shift1)
     (conv3 of one bottleneck block + conv1 of the next, cirtorch/backbones/misc.py:166-203).
+    shortcut = residual, or with residual=None and proj=(xp, wp, scalep, shiftp) the block's 1x1
+    projection proj_bn(proj_conv(xp)) computed in the same pass.
     x: [N, H, W, 64] bf16, PERM32-packed weights; returns (y [N, H, W, 256], z [N, H, W, c_out])."""
     E.require_gpu(x, w3, residual, w1)
     n, h, w, c = x.shape
     c_mid = w3.shape[0]
     y = torch.empty((n, h, w, c_mid), dtype=x.dtype, device=x.device)
     z = torch.empty((n, h, w, c_out), dtype=x.dtype, device=x.device)
-    assert residual.shape == y.shape and residual.dtype == x.dtype and residual.is_contiguous() and x.is_contiguous()
+    assert x.is_contiguous()
+    if residual is not None:
+        assert residual.shape == y.shape and residual.dtype == x.dtype and residual.is_contiguous()
+        xp = wp = sp = hp = None
+    else:
+        xp, wp, sp, hp = proj
+        E.require_gpu(xp, wp, sp, hp)
+        assert xp.shape == x.shape and xp.dtype == x.dtype and xp.is_contiguous()
     E.check(E.lib().rr_conv1x1_pair(E.ptr(x), n * h * w, c, E.ptr(w3), E.ptr(scale3), E.ptr(shift3), c_mid,
-                                    E.ptr(residual), E.RR_ACT_LEAKY if leaky3 else E.RR_ACT_IDENTITY, float(slope3),
+                                    E.ptr(residual), E.ptr(xp), E.ptr(wp), E.ptr(sp), E.ptr(hp),
+                                    E.RR_ACT_LEAKY if leaky3 else E.RR_ACT_IDENTITY, float(slope3),
                                     E.ptr(w1), E.ptr(scale1), E.ptr(shift1), c_out,
                                     E.RR_ACT_LEAKY if leaky1 else E.RR_ACT_IDENTITY, float(slope1), E.ptr(y), E.ptr(z),
                                     E.dtype_code(x.dtype), _st()), "rr_conv1x1_pair")

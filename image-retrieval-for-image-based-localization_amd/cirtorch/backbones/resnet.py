@@ -221,21 +221,30 @@ class ResNet(nn.Module):
         flat = [(mod_id, steps, proj) for mod_id, blocks in enumerate(plan["mods"]) for steps, proj in blocks]
         pending = None  # conv1 output of the next block, produced by a fused boundary launch
         for i, (mod_id, steps, proj) in enumerate(flat):
-            res = self._conv(t, proj) if proj is not None else t
+            nxt = flat[i + 1][1][0] if i + 1 < len(flat) else None
+            pair = self._pairable(steps[-1], nxt)
+            fuse_proj = pair and proj is not None and self._proj_fusable(proj)
+            res = t if proj is None else (None if fuse_proj else self._conv(t, proj))
             y = t
             for j, st in enumerate(steps[:-1]):
                 y = pending if (j == 0 and pending is not None) else self._conv(y, st)
             pending = None
-            nxt = flat[i + 1][1][0] if i + 1 < len(flat) else None
-            if self._pairable(steps[-1], nxt):
+            if pair:
                 last = steps[-1]
                 t, pending = _ops.conv1x1_pair(y, last.w, last.scale, last.shift, res, last.leaky, last.slope,
-                                               nxt.w, nxt.scale, nxt.shift, nxt.c_out, nxt.leaky, nxt.slope)
+                                               nxt.w, nxt.scale, nxt.shift, nxt.c_out, nxt.leaky, nxt.slope,
+                                               proj=(t, proj.w, proj.scale, proj.shift) if fuse_proj else None)
             else:
                 t = self._conv(y, steps[-1], residual=res)
             if i + 1 == len(flat) or flat[i + 1][0] != mod_id:
                 outs["mod%d" % (mod_id + 2)] = t
         return OrderedDict((k, v.permute(0, 3, 1, 2)) for k, v in outs.items())
+
+    @staticmethod
+    def _proj_fusable(proj):
+        """stride-1 1x1 projection 64 -> 256 (first block of the 256-channel stage), identity activation"""
+        return (proj.kh == 1 and proj.stride == 1 and proj.pad == 0 and proj.perm and proj.c_out == 256
+                and proj.w.shape[1] == 64 and not proj.leaky)
 
     def _pairable(self, last, nxt):
         """conv3 of a 64->256 bottleneck followed by a stride-1 1x1 conv1 (256 -> 64/128):

@@ -220,11 +220,18 @@ __global__ void __launch_bounds__(64 * NW) k_stream1x1(ConvArgs a, int nslices) 
 // re-read from HBM (-2 B x 256 per pixel vs two launches).  Both weight slices
 // (32 KiB + C1 x 512 B) and the affines stay in LDS; activations stream
 // HBM -> VGPR D strips deep as in k_stream1x1.
+// PROJ: the first block of the stage, whose shortcut is the projection
+// proj_bn(proj_conv(x_in)) (1x1, stride 1, 64 -> 256): it is computed in the
+// same pass from the block input (a third GEMM into its own accumulators), so
+// the 256-channel projection map is neither written nor read back.
 struct PairArgs {
     const bf16_t* x;   // [P][64]
     const bf16_t* w3;  // [256][64]  PERM32 rows
     const float *s3, *h3;
-    const bf16_t* res; // [P][256]
+    const bf16_t* res; // [P][256] (!PROJ)
+    const bf16_t* xp;  // [P][64]  block input (PROJ)
+    const bf16_t* wp;  // [256][64] PERM32 rows (PROJ)
+    const float *sp, *hp;
     const bf16_t* w1;  // [C1][256]  PERM32 rows
     const float *s1, *h1;
     bf16_t* y;         // [P][256]
@@ -234,13 +241,15 @@ struct PairArgs {
     float slope3, slope1;
 };
 
-template <int C1, int D>
+template <int C1, int D, bool PROJ>
 __global__ void __launch_bounds__(512) k_stream_pair(PairArgs a) {
     constexpr int K3 = 64, C3 = 256, NW = 8;
     constexpr int NK3 = K3 / 32, NR3 = C3 / 32, NF1 = C1 / 16, NK1 = C3 / 32;
     __shared__ __attribute__((aligned(16))) char sW3[C3 * K3 * 2];
     __shared__ __attribute__((aligned(16))) char sW1[C1 * C3 * 2];
     __shared__ __attribute__((aligned(16))) float sS3[C3], sH3[C3], sS1[C1], sH1[C1];
+    __shared__ __attribute__((aligned(16))) char sWp[PROJ ? C3 * K3 * 2 : 16];
+    __shared__ __attribute__((aligned(16))) float sSp[PROJ ? C3 : 1], sHp[PROJ ? C3 : 1];
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -260,6 +269,16 @@ __global__ void __launch_bounds__(512) k_stream_pair(PairArgs a) {
         sS1[i] = a.s1[i];
         sH1[i] = a.h1[i];
     }
+    if constexpr (PROJ) {
+        for (int i = tid; i < C3 * K3 / 8; i += 64 * NW) {
+            const int r = i / (K3 / 8), c = i - r * (K3 / 8);
+            *reinterpret_cast<uint4*>(sWp + wswz<K3>(r, c)) = reinterpret_cast<const uint4*>(a.wp)[i];
+        }
+        for (int i = tid; i < C3; i += 64 * NW) {
+            sSp[i] = a.sp[i];
+            sHp[i] = a.hp[i];
+        }
+    }
     __syncthreads();
 
     const int r16 = lane & 15, kq = lane >> 4;
@@ -276,15 +295,21 @@ __global__ void __launch_bounds__(512) k_stream_pair(PairArgs a) {
         return p < P ? p : P - 1;
     };
 
-    uint4 bq[D][NK3], rq[D][NR3];
+    uint4 bq[D][NK3], rq[D][PROJ ? NK3 : NR3];  // PROJ: rq holds the block input's B fragments
     auto load = [&](int d, int s) {
         const long long p = pix(s);
         const bf16_t* xs = a.x + p * K3 + 8 * kq;
 #pragma unroll
         for (int kk = 0; kk < NK3; ++kk) bq[d][kk] = *reinterpret_cast<const uint4*>(xs + kk * 32);
-        const bf16_t* rs = a.res + p * C3 + 8 * kq;
+        if constexpr (PROJ) {
+            const bf16_t* ps = a.xp + p * K3 + 8 * kq;
 #pragma unroll
-        for (int i2 = 0; i2 < NR3; ++i2) rq[d][i2] = *reinterpret_cast<const uint4*>(rs + 32 * i2);
+            for (int kk = 0; kk < NK3; ++kk) rq[d][kk] = *reinterpret_cast<const uint4*>(ps + kk * 32);
+        } else {
+            const bf16_t* rs = a.res + p * C3 + 8 * kq;
+#pragma unroll
+            for (int i2 = 0; i2 < NR3; ++i2) rq[d][i2] = *reinterpret_cast<const uint4*>(rs + 32 * i2);
+        }
     };
 #pragma unroll
     for (int d = 0; d < D; ++d) load(d, strip_of(d));
@@ -312,18 +337,36 @@ __global__ void __launch_bounds__(512) k_stream_pair(PairArgs a) {
                                                                          acc[h], 0, 0, 0);
                     }
                 const int c = 32 * i2 + 8 * kq;
-                const uint4 q = rq[d][i2];
-                const unsigned w4[4] = {q.x, q.y, q.z, q.w};
                 float v[8];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     v[r] = acc[0][r] * sS3[c + r] + sH3[c + r];
                     v[4 + r] = acc[1][r] * sS3[c + 4 + r] + sH3[c + 4 + r];
                 }
+                if constexpr (PROJ) {  // shortcut = proj_bn(proj_conv(x_in)), kept in f32
+                    sf32x4_t pacc[2] = {(sf32x4_t){0.f, 0.f, 0.f, 0.f}, (sf32x4_t){0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    v[2 * r] += __uint_as_float(w4[r] << 16);
-                    v[2 * r + 1] += __uint_as_float(w4[r] & 0xffff0000u);
+                    for (int kk = 0; kk < NK3; ++kk)
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            const uint4 av = *reinterpret_cast<const uint4*>(sWp + abase + wswz<K3>((2 * i2 + h) * 16 + r16, kk * 4 + kq));
+                            pacc[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(sbf16x8_t, av),
+                                                                              __builtin_bit_cast(sbf16x8_t, rq[d][kk]),
+                                                                              pacc[h], 0, 0, 0);
+                        }
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        v[r] += pacc[0][r] * sSp[c + r] + sHp[c + r];
+                        v[4 + r] += pacc[1][r] * sSp[c + 4 + r] + sHp[c + 4 + r];
+                    }
+                } else {
+                    const uint4 q = rq[d][i2];
+                    const unsigned w4[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        v[2 * r] += __uint_as_float(w4[r] << 16);
+                        v[2 * r + 1] += __uint_as_float(w4[r] & 0xffff0000u);
+                    }
                 }
                 if (leaky3) {
 #pragma unroll
@@ -424,14 +467,20 @@ bool launch_stream1x1(const ConvArgs& a, hipStream_t s) {
 using namespace rr;
 
 extern "C" int rr_conv1x1_pair(const void* x, long long p, int c_in, const void* w3, const float* scale3,
-                               const float* shift3, int c_mid, const void* residual, int act3, float slope3,
-                               const void* w1, const float* scale1, const float* shift1, int c_out, int act1,
-                               float slope1, void* y, void* z, int dtype, void* stream) {
+                               const float* shift3, int c_mid, const void* residual, const void* xp, const void* wp,
+                               const float* scalep, const float* shiftp, int act3, float slope3, const void* w1,
+                               const float* scale1, const float* shift1, int c_out, int act1, float slope1, void* y,
+                               void* z, int dtype, void* stream) {
     if (dtype != RR_BF16) return fail(RR_EINVAL, "rr_conv1x1_pair: bf16 only");
     if (c_in != 64 || c_mid != 256 || (c_out != 64 && c_out != 128))
         return fail(RR_EINVAL, "rr_conv1x1_pair: shapes (c_in 64, c_mid 256, c_out 64|128) only");
-    if (!x || !w3 || !scale3 || !shift3 || !residual || !w1 || !scale1 || !shift1 || !y || !z)
+    if (!x || !w3 || !scale3 || !shift3 || !w1 || !scale1 || !shift1 || !y || !z)
         return fail(RR_EINVAL, "rr_conv1x1_pair: null pointer");
+    const bool proj = residual == nullptr;
+    if (proj && (!xp || !wp || !scalep || !shiftp))
+        return fail(RR_EINVAL, "rr_conv1x1_pair: either residual or the projection (xp, wp, scalep, shiftp) is required");
+    if (proj && ((((uintptr_t)xp) | ((uintptr_t)wp)) & 15))
+        return fail(RR_EINVAL, "rr_conv1x1_pair: 16-byte alignment required");
     if (p <= 0) return fail(RR_EINVAL, "rr_conv1x1_pair: empty");
     if ((((uintptr_t)x) | ((uintptr_t)residual) | ((uintptr_t)y) | ((uintptr_t)z) | ((uintptr_t)w3) |
          ((uintptr_t)w1)) & 15)
@@ -443,12 +492,15 @@ extern "C" int rr_conv1x1_pair(const void* x, long long p, int c_in, const void*
     a.x = (const bf16_t*)x; a.w3 = (const bf16_t*)w3; a.s3 = scale3; a.h3 = shift3; a.res = (const bf16_t*)residual;
     a.w1 = (const bf16_t*)w1; a.s1 = scale1; a.h1 = shift1; a.y = (bf16_t*)y; a.z = (bf16_t*)z; a.P = p;
     a.act3 = act3; a.act1 = act1; a.slope3 = slope3; a.slope1 = slope1;
+    a.xp = (const bf16_t*)xp; a.wp = (const bf16_t*)wp; a.sp = scalep; a.hp = shiftp;
     const long long nstrips = (p + 15) / 16;
     long long grid = (nstrips + 7) / 8;
     if (grid > g_pair_cus) grid = g_pair_cus;
-    if (c_out == 64)
-        hipLaunchKernelGGL((k_stream_pair<64, 2>), dim3((unsigned)grid), dim3(512), 0, as_stream(stream), a);
-    else
-        hipLaunchKernelGGL((k_stream_pair<128, 2>), dim3((unsigned)grid), dim3(512), 0, as_stream(stream), a);
+    const dim3 g((unsigned)grid), b(512);
+    hipStream_t s = as_stream(stream);
+    if (c_out == 64 && !proj) hipLaunchKernelGGL((k_stream_pair<64, 2, false>), g, b, 0, s, a);
+    else if (c_out == 64) hipLaunchKernelGGL((k_stream_pair<64, 2, true>), g, b, 0, s, a);
+    else if (!proj) hipLaunchKernelGGL((k_stream_pair<128, 2, false>), g, b, 0, s, a);
+    else hipLaunchKernelGGL((k_stream_pair<128, 2, true>), g, b, 0, s, a);
     return check_launch("rr_conv1x1_pair");
 }

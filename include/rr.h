@@ -92,17 +92,21 @@ int rr_pack_conv_weights(const float* w, int c_out, int c_in, int kh, int kw, in
                          int k_packed, int perm32, void* out, int dtype, void* stream);
 
 /* Fused bottleneck boundary, bf16, PERM32-packed weights (1x1 convs):
- *   y = act3(conv1x1(x, w3) * scale3 + shift3 + residual)      [p][c_mid]
+ *   y = act3(conv1x1(x, w3) * scale3 + shift3 + shortcut)      [p][c_mid]
  *   z = act1(conv1x1(y, w1) * scale1 + shift1)                 [p][c_out]
  * i.e. conv3 + bn3 + residual add + activation of ResidualBlock i and conv1 +
  * bn1 + activation of block i + 1 (cirtorch/backbones/misc.py:166-203), in one
- * pass that never re-reads y.  p = pixels (n*h*w, stride 1).  Shapes: c_in 64,
+ * pass that never re-reads y.  shortcut = residual ([p][c_mid]) when given;
+ * with residual == NULL it is the block's projection proj_bn(proj_conv(xp))
+ * (1x1 stride 1, xp [p][c_in], wp [c_mid][c_in], scalep/shiftp; misc.py:179-182)
+ * computed in the same pass.  p = pixels (n*h*w, stride 1).  Shapes: c_in 64,
  * c_mid 256, c_out 64 or 128 (the 256-channel stage); anything else returns
- * RR_EINVAL and the caller runs the two rr_conv2d_fused launches instead. */
+ * RR_EINVAL and the caller runs separate rr_conv2d_fused launches instead. */
 int rr_conv1x1_pair(const void* x, long long p, int c_in, const void* w3, const float* scale3,
-                    const float* shift3, int c_mid, const void* residual, int act3, float slope3,
-                    const void* w1, const float* scale1, const float* shift1, int c_out, int act1,
-                    float slope1, void* y, void* z, int dtype, void* stream);
+                    const float* shift3, int c_mid, const void* residual, const void* xp, const void* wp,
+                    const float* scalep, const float* shiftp, int act3, float slope3, const void* w1,
+                    const float* scale1, const float* shift1, int c_out, int act1, float slope1, void* y,
+                    void* z, int dtype, void* stream);
 
 /* 3x3/s2/p1 style max pooling, NHWC.  Replaces nn.MaxPool2d(3, stride=2,
  * padding=1) of the stem (cirtorch/backbones/resnet.py:65). */

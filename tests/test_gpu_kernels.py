@@ -298,3 +298,40 @@ def test_conv1x1_pair(cuda, c_out, shape):
     z2 = ops.conv2d_fused(y2, w1p, 1, 1, 1, 0, c_out, c[2], c[3], leaky=True, perm32=True)
     assert torch.equal(y.cpu(), y2.cpu())
     assert (z.float() == z2.float()).float().mean().item() > 0.99
+
+
+@pytest.mark.parametrize("c_out", [64, 128])
+def test_conv1x1_pair_projection(cuda, c_out):
+    """First block of the stage: the shortcut is proj_bn(proj_conv(x_in))
+    (cirtorch/backbones/misc.py:179-182), computed inside the fused launch."""
+    n, h, w = 2, 19, 29
+    g = torch.Generator().manual_seed(c_out + 3)
+    ops = _ops()
+    x = _bf16_round(torch.randn(n, 64, h, w, generator=g))
+    xin = _bf16_round(torch.randn(n, 64, h, w, generator=g))
+    w3 = _bf16_round(torch.randn(256, 64, 1, 1, generator=g) * (2.0 / 64) ** 0.5)
+    wpj = _bf16_round(torch.randn(256, 64, 1, 1, generator=g) * (2.0 / 64) ** 0.5)
+    w1 = _bf16_round(torch.randn(c_out, 256, 1, 1, generator=g) * (2.0 / 256) ** 0.5)
+    s3, h3 = torch.rand(256, generator=g) + 0.5, torch.randn(256, generator=g) * 0.1
+    sp, hp = torch.rand(256, generator=g) + 0.5, torch.randn(256, generator=g) * 0.1
+    s1, h1 = torch.rand(c_out, generator=g) + 0.5, torch.randn(c_out, generator=g) * 0.1
+
+    def col(v):
+        return v.double()[None, :, None, None]
+
+    def nhwc(t):
+        return t.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(cuda)
+
+    short = F.conv2d(xin.double(), wpj.double()) * col(sp) + col(hp)
+    yr = F.leaky_relu(F.conv2d(x.double(), w3.double()) * col(s3) + col(h3) + short, 0.01)
+    zr = F.leaky_relu(F.conv2d(_bf16_round(yr.float()).double(), w1.double()) * col(s1) + col(h1), 0.01)
+    bf = torch.bfloat16
+    w3p = ops.pack_conv_weights(w3.to(cuda), 64, bf, perm32=True)
+    wpp = ops.pack_conv_weights(wpj.to(cuda), 64, bf, perm32=True)
+    w1p = ops.pack_conv_weights(w1.to(cuda), 256, bf, perm32=True)
+    y, z = ops.conv1x1_pair(nhwc(x), w3p, s3.to(cuda), h3.to(cuda), None, True, 0.01, w1p, s1.to(cuda), h1.to(cuda),
+                            c_out, True, 0.01, proj=(nhwc(xin), wpp, sp.to(cuda), hp.to(cuda)))
+    gy = y.float().permute(0, 3, 1, 2).cpu().double()
+    gz = z.float().permute(0, 3, 1, 2).cpu().double()
+    assert (gy - yr).abs().max().item() <= 8e-3 * yr.abs().max().item()
+    assert (gz - zr).abs().max().item() <= 1.6e-2 * zr.abs().max().item()
