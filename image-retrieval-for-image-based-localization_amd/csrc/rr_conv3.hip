@@ -57,6 +57,17 @@ template <int N>
 __device__ __forceinline__ void pwait_barrier() {
     asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"(N) : "memory");
 }
+// vmcnt(n) + barrier for a wave-uniform runtime n <= N (a chain of scalar
+// compares picks the exact immediate).
+template <int N>
+__device__ __forceinline__ void pwait_barrier_n(int n) {
+    if constexpr (N == 0) {
+        pwait_barrier<0>();
+    } else {
+        if (n >= N) pwait_barrier<N>();
+        else pwait_barrier_n<N - 1>(n);
+    }
+}
 
 __device__ __forceinline__ pi32x4_t prsrc(const void* base, unsigned bytes) {
     const unsigned long long b = (unsigned long long)base;
@@ -72,7 +83,7 @@ struct TileC {
     int ct, img, oh0, ow0;
 };
 
-template <int TC, int TH, int TW, int WC, int WP, bool ARES>
+template <int TC, int TH, int TW, int WC, int WP, bool ARES, int NSA>
 __global__ void __launch_bounds__(64 * WC * WP) k_conv3x3(ConvArgs a, int tiles_w, int tiles_hw, int tiles_c,
                                                          int ntiles) {
     constexpr int NW = WC * WP, NT = 64 * NW;
@@ -83,13 +94,14 @@ __global__ void __launch_bounds__(64 * WC * WP) k_conv3x3(ConvArgs a, int tiles_
     constexpr int PBYTES = (ARES ? NDP : NDPW * NW) * 1024;
     constexpr int NIA = TC / (8 * NW);           // weight wave-instructions per wave per K-step
     constexpr int AST = TC * 128;                // one weight K-step in LDS
-    constexpr int ABYTES = (ARES ? 9 : 2) * AST;
+    constexpr int ABYTES = (ARES ? 9 : NSA) * AST;
     constexpr int MAXC = ARES ? TC : 512;        // BN scale/shift of every output channel
     constexpr int FM = TC / WC / 16, FN = TP / WP / 16;
     constexpr int NST = (FM / 2) * FN;           // epilogue stores per wave (full tiles only)
     static_assert(TC % (8 * NW) == 0 && FM % 2 == 0 && TW % 16 == 0 && (TP / WP) % 16 == 0, "tile shape");
     static_assert(ARES || NDPW <= 8, "ring mode fetches the next patch one piece per tap (taps 0..7)");
     static_assert(NST >= 2, "vmcnt immediates below assume NST > 1");
+    static_assert(NSA == 2 || NSA == 3, "weight ring depth");
     __shared__ __attribute__((aligned(1024))) char smem[ABYTES + 2 * PBYTES + 2 * MAXC * 4];
     float* sS = reinterpret_cast<float*>(smem + ABYTES + 2 * PBYTES);
     float* sH = sS + MAXC;
@@ -250,27 +262,38 @@ __global__ void __launch_bounds__(64 * WC * WP) k_conv3x3(ConvArgs a, int tiles_
             if (lt + 1 < my_tiles) cur = tile_of(lt + 1);
         }
     } else {
-        // steps (tile, chunk, tap); weight K-steps through a 2-stage ring, one
+        // steps (tile, chunk, tap); weight K-steps through an NSA-stage ring, one
         // barrier per step; the next (tile, chunk) patch arrives piecewise.
         const int total = my_tiles * nck * 9;
         TileC nxt = my_tiles > 1 ? tile_of(1) : cur;
-        for (int d = wave; d < NDP; d += NW) patch_dma(cur, 0, 0, d);
-        w_dma(cur.ct, 0, 0, lds0);
-        int lt = 0, cc = 0, tap = 0, grp = 0, after = 0;
-        for (int s = 0; s < total; ++s) {
-            // A(s) landed: only `after` younger VMEM ops (a patch piece, the
-            // previous tile's epilogue stores) may stay in flight
-            if (after == 0) pwait_barrier<0>();
-            else if (after == 1) pwait_barrier<1>();
-            else if (after == NST) pwait_barrier<NST>();
-            else pwait_barrier<NST + 1>();
-            int ntap = tap + 1, ncc = cc, nlt = lt;
-            if (ntap == 9) {
-                ntap = 0;
-                if (++ncc == nck) { ncc = 0; ++nlt; }
+        auto adv = [&](int& t_, int& c_, int& l_) {
+            if (++t_ == 9) {
+                t_ = 0;
+                if (++c_ == nck) { c_ = 0; ++l_; }
             }
-            after = 0;
-            if (s + 1 < total) w_dma(nlt == lt ? cur.ct : nxt.ct, ntap, ncc, lds0 + ((s + 1) & 1) * AST);
+        };
+        for (int d = wave; d < NDP; d += NW) patch_dma(cur, 0, 0, d);
+        int ptap = 0, pcc = 0, plt = 0;  // next weight K-step to fetch
+        for (int i = 0; i < NSA - 1 && i < total; ++i) {
+            w_dma(plt == 0 ? cur.ct : nxt.ct, ptap, pcc, lds0 + i * AST);
+            adv(ptap, pcc, plt);
+        }
+        int lt = 0, cc = 0, tap = 0, grp = 0;
+        int tm1 = 0, tm2 = 0, am1 = 0;  // VMEM ops after the weight fetch of steps s-1, s-2; weight ops of s-1
+        for (int s = 0; s < total; ++s) {
+            // A(s) landed; only the younger VMEM ops (later weight steps, patch
+            // pieces, the previous tile's epilogue stores) may stay in flight
+            if (s == 0) pwait_barrier<0>();
+            else if constexpr (NSA == 2) pwait_barrier_n<NST + 1>(tm1);
+            else pwait_barrier_n<NIA + NST + 2>(tm2 + am1 + tm1);
+            int ntap = tap, ncc = cc, nlt = lt;
+            adv(ntap, ncc, nlt);
+            int a_now = 0, t_now = 0;
+            if (s + NSA - 1 < total) {  // weight K-step s + NSA - 1 into the slot step s - 1 used
+                w_dma(plt == lt ? cur.ct : nxt.ct, ptap, pcc, lds0 + ((s + NSA - 1) % NSA) * AST);
+                adv(ptap, pcc, plt);
+                a_now = NIA;
+            }
             if (tap < NDPW) {  // piece `tap` of the next group's patch
                 const bool same = cc + 1 < nck;
                 if (same || lt + 1 < my_tiles) {
@@ -280,19 +303,22 @@ __global__ void __launch_bounds__(64 * WC * WP) k_conv3x3(ConvArgs a, int tiles_
                     g.oh0 = same ? cur.oh0 : nxt.oh0;
                     g.ow0 = same ? cur.ow0 : nxt.ow0;
                     patch_dma(g, same ? cc + 1 : 0, (grp + 1) & 1, wave + NW * tap);
-                    after = 1;
+                    t_now = 1;
                 }
             }
-            mfma_step(smem + (s & 1) * AST, smem + ABYTES + (grp & 1) * PBYTES, (tap / 3) * PC + tap % 3);
+            mfma_step(smem + (s % NSA) * AST, smem + ABYTES + (grp & 1) * PBYTES, (tap / 3) * PC + tap % 3);
             if (ntap == 0) {
                 ++grp;
                 if (ncc == 0) {
                     epilogue(cur);
-                    after += NST;
+                    t_now += NST;
                     cur = nxt;
                     if (nlt + 1 < my_tiles) nxt = tile_of(nlt + 1);
                 }
             }
+            tm2 = tm1;
+            tm1 = t_now;
+            am1 = a_now;
             tap = ntap;
             cc = ncc;
             lt = nlt;
@@ -300,20 +326,20 @@ __global__ void __launch_bounds__(64 * WC * WP) k_conv3x3(ConvArgs a, int tiles_
     }
 }
 
-template <int TC, int TH, int TW, int WC, int WP, bool ARES>
+template <int TC, int TH, int TW, int WC, int WP, bool ARES, int NSA = 2>
 void launch_c3(const ConvArgs& a, hipStream_t s) {
     const int tiles_w = a.w_ / TW, tiles_h = a.h / TH, tiles_c = a.cout / TC;
     const long long ntl = (long long)a.n * tiles_h * tiles_w * tiles_c;
     const int cus = grid_cus();
     const int grid = (int)(ntl < cus ? ntl : cus);
-    hipLaunchKernelGGL((k_conv3x3<TC, TH, TW, WC, WP, ARES>), dim3(grid), dim3(64 * WC * WP), 0, s, a, tiles_w,
+    hipLaunchKernelGGL((k_conv3x3<TC, TH, TW, WC, WP, ARES, NSA>), dim3(grid), dim3(64 * WC * WP), 0, s, a, tiles_w,
                        tiles_w * tiles_h, tiles_c, (int)ntl);
 }
 
 }  // namespace
 
 int g_conv3_mode = 1;  // rr_set_tuning(RR_TUNE_CONV3X3): 0 off, 1 auto, 2 / 3 prefer 8x32 / 4x32 tiles,
-                       // 4 / 6 A-stationary with 1x8 / 1x4 waves (auto: 2x4)
+                       // 4 / 6 A-stationary with 1x8 / 1x4 waves (auto: 2x4), 7 3-stage weight ring
 
 // bf16 3x3 / stride 1 / pad 1 with PERM32 weights, bf16 out, no residual, and
 // image sizes the tiles divide; returns false otherwise (caller falls back to
@@ -338,12 +364,15 @@ bool launch_conv3x3(const ConvArgs& a, hipStream_t s) {
         // (tuning modes 2 / 3 force one of them where the image height allows)
         const long long t8 = a.h % 8 == 0 ? (long long)a.n * (a.h / 8) * (a.w_ / 32) * (a.cout / 128) : 0;
         const bool want8 = g_conv3_mode == 2 || (g_conv3_mode != 3 && t8 >= 2 * g_c3_cus);
+        const bool deep = g_conv3_mode == 7;  // 3-stage weight ring
         if (t8 > 0 && (want8 || a.h % 4 != 0)) {
-            launch_c3<128, 8, 32, 2, 4, false>(a, s);
+            if (deep) launch_c3<128, 8, 32, 2, 4, false, 3>(a, s);
+            else launch_c3<128, 8, 32, 2, 4, false>(a, s);
             return true;
         }
         if (a.h % 4 == 0) {
-            launch_c3<128, 4, 32, 2, 4, false>(a, s);
+            if (deep) launch_c3<128, 4, 32, 2, 4, false, 3>(a, s);
+            else launch_c3<128, 4, 32, 2, 4, false>(a, s);
             return true;
         }
     }

@@ -557,6 +557,8 @@ void launch_gemm2(const ConvArgs& a, bool k1, hipStream_t s) {
         case 3: launch_cfg3<T, TO, 256, 128, 4, 2>(a, k1, perm, s); return;
         case 4: launch_cfg3<T, TO, 256, 256, 4, 2>(a, k1, perm, s); return;
         case 5: launch_cfg3<T, TO, 256, 64, 4, 1>(a, k1, perm, s); return;
+        case 7: launch_ns<T, TO, 256, 128, 4, 2, 3>(a, k1, perm, s); return;  // 8 waves, 3-stage ring (144 KiB)
+        case 8: launch_ns<T, TO, 128, 256, 2, 4, 3>(a, k1, perm, s); return;  // 8 waves, 3-stage ring (144 KiB)
         default: break;
     }
     // A-stationary variants (single output-channel tile, short K)
@@ -576,6 +578,8 @@ void launch_gemm2(const ConvArgs& a, bool k1, hipStream_t s) {
         launch_cfg3<T, TO, 256, 32, 4, 1>(a, k1, perm, s);
     else if (a.P <= 64)
         launch_cfg3<T, TO, 256, 64, 4, 1>(a, k1, perm, s);
+    else if (a.P <= 128 && a.cout >= 4096)  // kNN score GEMM at 65..128 queries: no half-empty 256-wide pixel tiles
+        launch_cfg3<T, TO, 256, 128, 4, 2>(a, k1, perm, s);
     else if (a.cout <= 64)
         launch_cfg3<T, TO, 64, 256, 1, 4>(a, k1, perm, s);
     else if (a.cout <= 128 || !g_wide)

@@ -184,7 +184,8 @@ int rr_topk_merge(const double* in_scores, const long long* in_idx, int r, int n
 /* ------------------------------------------------------------ tuning */
 /* Engine tuning knobs (process-wide; for benchmarking / autotuning tools):
  *   RR_TUNE_GEMM_CONFIG  0 = automatic tile choice, 1 = 128x128, 2 = 64x256,
- *                        3 = 256x128 (8 waves), 4 = 256x256 (8 waves), 5 = 256x64
+ *                        3 = 256x128 (8 waves), 4 = 256x256 (8 waves), 5 = 256x64,
+ *                        7 / 8 = 256x128 / 128x256 (8 waves, 3-stage ring)
  *                        6 = A-stationary (weights resident in LDS) where eligible
  *   RR_TUNE_GEMM_STAGES  2 or 3 LDS stages (3: one resident block per CU)
  *   RR_TUNE_GEMM_WIDE    0/1 allow the 8-wave tiles in the automatic choice
@@ -195,7 +196,8 @@ int rr_topk_merge(const double* in_scores, const long long* in_idx, int r, int n
  *   RR_TUNE_CONV3X3      0 off, 1 auto (default): direct 3x3 kernel with LDS
  *                        halo patches for the bf16 stride-1 3x3 convs;
  *                        2 / 3 prefer its 8x32 / 4x32 pixel tiles, 4 / 6 use
- *                        1x8 / 1x4 waves for the c_in = 64 A-stationary form
+ *                        1x8 / 1x4 waves for the c_in = 64 A-stationary form,
+ *                        7 a 3-stage weight ring
  *   RR_TUNE_GRID_CUS     cap on the CUs one persistent launch spreads over
  *                        (0 = all; e.g. half the chip for two concurrent streams) */
 enum rr_tune_key { RR_TUNE_GEMM_CONFIG = 0, RR_TUNE_GEMM_STAGES = 1, RR_TUNE_GEMM_WIDE = 2,

@@ -46,7 +46,7 @@ TILE_CASES = CONV_CASES + [
 ]
 
 
-@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("case", TILE_CASES)
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
 def test_conv_tile_configs(cuda, cfg, case, prec):
@@ -98,7 +98,7 @@ CONV3_CASES = [
 
 
 @pytest.mark.parametrize("case", CONV3_CASES)
-@pytest.mark.parametrize("mode", [1, 2, 3, 4, 6, 0])
+@pytest.mark.parametrize("mode", [1, 2, 3, 4, 6, 7, 0])
 def test_conv3x3_direct(cuda, case, mode):
     """Direct 3x3 kernel (modes 1-4, 6: auto / 8x32 / 4x32 tiles / A-stationary wave layouts) and the
     implicit-GEMM fallback (mode 0) against the float64 reference."""

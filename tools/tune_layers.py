@@ -14,7 +14,7 @@ sys.path.insert(0, REPO)
 
 import torch  # noqa: E402
 
-CFG = {1: "128x128", 2: "64x256", 3: "256x128w", 4: "256x256w", 5: "256x64", 6: "A-stat"}
+CFG = {1: "128x128", 2: "64x256", 3: "256x128w", 4: "256x256w", 5: "256x64", 6: "A-stat", 7: "256x128w3", 8: "128x256w3"}
 
 
 def main():
