@@ -37,9 +37,12 @@ def main():
     print("Extractor-body kernel family (%s): %.1f us of kernel time per %d-image forward "
           "(sum of rocprof durations / %d forwards); bench HIP-event body time per forward: %.1f us "
           "(includes launch gaps)." % (", ".join(BODY), body_us, eb, args.forwards, per_fwd_bench))
-    print("Per-family averages: " + "; ".join("%s %.1f us x %s" % (r["Name"].split("(")[0][-60:],
-                                                                 float(r["AverageNs"]) / 1e3, r["Calls"])
-                                               for r in body[:12]))
+    print()
+    print("| body kernel | avg us | calls in run | us per forward |\n|---|---|---|---|")
+    for r in body:
+        name = r["Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
+        print("| `%s` | %.1f | %s | %.1f |" % (name, float(r["AverageNs"]) / 1e3, r["Calls"],
+                                            float(r["TotalDurationNs"]) / 1e3 / args.forwards))
 
 
 if __name__ == "__main__":
