@@ -57,6 +57,7 @@ def parse():
     ap.add_argument("--knn-q", type=int, default=1024, help="queries for the kNN-only sub-benchmark (0 = skip)")
     ap.add_argument("--knn-steps", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--local-kpts", type=int, default=2048, help="keypoints per image for the local-head sub-benchmark (0 = skip)")
     ap.add_argument("--overlap", action="store_true",
                     help="run batch i's match on a second stream, overlapping batch i+1's extract (measured slower on one GPU)")
     ap.add_argument("--cpu-images", type=int, default=2)
@@ -289,6 +290,38 @@ def main():
             traffic_note = ("HBM bytes of the step's extractor dispatches from rocprofv3 PMC (2 x FETCH_SIZE + "
                             "WRITE_SIZE, profiles/r01_pmc_traffic.json, %d-image forwards, commit %s)"
                             % (c.get("batch", 0), c.get("source_commit", "?")))
+    # local-descriptor head: 2048 keypoints per image on an
+    # R50 mod4-shaped bf16 map (1024 ch at H/16 x W/16), E = 128, + mutual NN of two images
+    local = None
+    if args.local_kpts > 0:
+        from cirtorch.search import mutual_nn
+        nb, c4, h4, w4 = 8, 1024, H // 16, W // 16
+        fmap = torch.randn((nb, h4, w4, c4), generator=g, device=dev).to(torch.bfloat16).permute(0, 3, 1, 2)
+        kp = torch.rand((nb, args.local_kpts, 2), generator=g, device=dev) * 2 - 1
+        wl = torch.randn((128, c4), generator=g, device=dev) * c4 ** -0.5
+        bl = torch.zeros(128, device=dev)
+        _ops.local_head(fmap, kp, wl, bl)
+        torch.cuda.synchronize()
+        ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ea.record()
+        for _ in range(10):
+            d = _ops.local_head(fmap, kp, wl, bl)
+        eb.record()
+        torch.cuda.synchronize()
+        t_head = ea.elapsed_time(eb) / 10 * 1e-3
+        mutual_nn(d[0], d[1])
+        torch.cuda.synchronize()
+        ea.record()
+        for _ in range(10):
+            mutual_nn(d[0], d[1])
+        eb.record()
+        torch.cuda.synchronize()
+        t_mnn = ea.elapsed_time(eb) / 10 * 1e-3
+        local = {"keypoints_per_sec": nb * args.local_kpts / t_head, "map": [nb, c4, h4, w4], "kpts": args.local_kpts,
+                 "embedding": 128, "ms_per_batch": t_head * 1e3, "mutual_nn_ms": t_mnn * 1e3,
+                 "note": "rr_local_head (bilinear sample + exact-f32 MFMA Linear + normalize) on a synthetic bf16 map; "
+                         "mutual_nn = two exact top-1 searches (%d x %d x 128) + rr_mutual_nn"
+                         % (args.local_kpts, args.local_kpts)}
     fl_img = conv_flops_per_image(net.body, H, W)
     costs = layer_costs(net.body, H, W, 2 if args.precision == "bf16" else 4)
     peak_m = (PEAK_BF16_TFLOPS if args.precision == "bf16" else PEAK_F32_TFLOPS) * 1e12
@@ -331,6 +364,7 @@ def main():
                                     "peak_hbm) for the step's images, over the measured extractor time"},
         "extract_images_per_sec": ext_only * world,
         "knn": knn,
+        "local": local,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args)

@@ -266,3 +266,36 @@ def cast_bf16(x):
     y = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
     E.check(E.lib().rr_cast_f32_bf16(E.ptr(x), E.ptr(y), x.numel(), _st()), "rr_cast_f32_bf16")
     return y
+
+
+# ---------------------------------------------------------------- local descriptors
+def local_head(x, kpts, weight, bias):
+    """x: [N, C, H, W] feature map (channels_last view or NHWC-able, f32/bf16), kpts [N, P, 2]
+    normalised (x, y) -> normalize(Linear(grid_sample(x, kpts))) as [N, P, E] float32
+    (cirtorch/modules/heads/local_head.py:43-71)."""
+    E.require_gpu(x, kpts, weight, bias)
+    n, c, h, w = x.shape
+    xh = x.permute(0, 2, 3, 1)
+    if not xh.is_contiguous():
+        xh = xh.contiguous()
+    if xh.dtype not in (torch.float32, torch.bfloat16):
+        xh = xh.float()
+    kp = kpts.contiguous().float()
+    npts = kp.shape[1]
+    wt = weight.contiguous().float()
+    b = bias.contiguous().float() if bias is not None else None
+    e = wt.shape[0]
+    out = torch.empty((n, npts, e), dtype=torch.float32, device=x.device)
+    ws = torch.empty(int(E.lib().rr_local_head_workspace_bytes(n * npts, c, e)), dtype=torch.uint8, device=x.device)
+    E.check(E.lib().rr_local_head(E.ptr(xh), n, h, w, c, E.dtype_code(xh.dtype), E.ptr(kp), npts, E.ptr(wt), E.ptr(b),
+                                  e, E.ptr(out), E.ptr(ws), ws.numel(), _st()), "rr_local_head")
+    return out
+
+
+def mutual_nn(nn12, nn21):
+    """int64 top-1 lists of both directions -> match [n1] (-1 where not mutual)."""
+    E.require_gpu(nn12, nn21)
+    a, b = nn12.contiguous().long(), nn21.contiguous().long()
+    out = torch.empty_like(a)
+    E.check(E.lib().rr_mutual_nn(E.ptr(a), a.numel(), E.ptr(b), b.numel(), E.ptr(out), _st()), "rr_mutual_nn")
+    return out

@@ -117,3 +117,15 @@ class ShardedIndex:
 def merge_topk(scores, idx, k):
     """[R, Q, k_in] per-shard lists -> [Q, k] by (score desc, index asc)."""
     return _ops.topk_merge(scores, idx, k)
+
+
+def mutual_nn(desc1, desc2, precision="fp32"):
+    """Mutual nearest-neighbour matcher of HPatchesEval.py:31-43 for unit-norm
+    descriptors [N1, D] and [N2, D] (rows): nearest by L2 distance == highest
+    dot product, exact order with ties to the lower index like np.argmin.
+    Returns int64 [N1]: the match in desc2, or -1 where not mutual."""
+    a = desc1.float().contiguous()
+    b = desc2.float().contiguous()
+    _, n12 = KnnIndex(b, precision).search(a, 1)
+    _, n21 = KnnIndex(a, precision).search(b, 1)
+    return _ops.mutual_nn(n12[:, 0], n21[:, 0])

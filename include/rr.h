@@ -181,6 +181,25 @@ int rr_knn_topk(const void* db, const float* db_f32, long long n_db,
 int rr_topk_merge(const double* in_scores, const long long* in_idx, int r, int nq, int k_in,
                   int k, double* out_scores, long long* out_idx, void* stream);
 
+/* ------------------------------------------------------- local descriptors */
+/* Local-descriptor head (config 5): desc = normalize(W . grid_sample(x, kpts) + b).
+ * Replaces cirtorch/modules/heads/local_head.py:43-71 (localHead.forward:
+ * functional.grid_sample(mode="bilinear", padding_mode="zeros",
+ * align_corners=False) -> nn.Linear(dim, e) -> functional.normalize(dim=2)).
+ *   x    : [n][h][w][c] NHWC feature map (dtype), c a multiple of 8 (bf16) / 4 (f32)
+ *   kpts : [n][npts][2] float32 normalised (x, y) in [-1, 1] (grid_sample grid)
+ *   weight [e][c], bias [e] (may be NULL) float32;  out [n][npts][e] float32
+ * workspace: rr_local_head_workspace_bytes(n*npts, c, e). */
+size_t rr_local_head_workspace_bytes(long long nkp, int c, int e);
+int rr_local_head(const void* x, int n, int h, int w, int c, int dtype, const float* kpts, int npts,
+                  const float* weight, const float* bias, int e, float* out, void* workspace,
+                  size_t workspace_bytes, void* stream);
+/* Mutual nearest neighbours from the two directions' top-1 lists (int64):
+ * match[i] = nn12[i] if nn21[nn12[i]] == i else -1.  Replaces the
+ * np.argmin/argmin mutual check of HPatchesEval.py:31-43 (nn12/nn21 from
+ * rr_knn_topk with k = 1: exact order, ties -> lower index like np.argmin). */
+int rr_mutual_nn(const long long* nn12, int n1, const long long* nn21, int n2, long long* match, void* stream);
+
 /* ------------------------------------------------------------ tuning */
 /* Engine tuning knobs (process-wide; for benchmarking / autotuning tools):
  *   RR_TUNE_GEMM_CONFIG  0 = automatic tile choice, 1 = 128x128, 2 = 64x256,

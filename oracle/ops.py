@@ -194,3 +194,26 @@ def pcawhitenlearn(X):
     eigval = eigval[order]
     eigvec = eigvec[:, order]
     return m, np.dot(np.linalg.inv(np.sqrt(np.diag(eigval))), eigvec.T)
+
+
+def local_head(x, kpts, w, b):
+    """localHead.forward (cirtorch/modules/heads/local_head.py:43-71): bilinear
+    grid_sample (zeros, align_corners=False; local_head.py:51) -> permute ->
+    Linear (:67) -> functional.normalize(dim=2) (:69).  x [B,C,H,W], kpts [B,N,2]."""
+    import torch.nn.functional as F
+    d = F.grid_sample(x, kpts.unsqueeze(2), mode="bilinear", padding_mode="zeros", align_corners=False)
+    d = d.squeeze(-1).permute(0, 2, 1)
+    return F.normalize(F.linear(d, w, b), dim=2)
+
+
+def nn_matcher(desc1, desc2):
+    """Mutual-NN matcher of HPatchesEval.py:23-43 (get_desc_dist + nn_matcher),
+    restated: L2 distance matrix, argmin both ways, -1 where not mutual.
+    (The reference module imports cv2, absent here: parity unpinned by a
+    reference run; the restatement is five numpy lines of the same calls.)"""
+    dist = np.linalg.norm(desc1[:, None] - desc2[None], axis=2)
+    n1 = np.argmin(dist, axis=1)
+    n2 = np.argmin(dist, axis=0)
+    n1 = n1.copy()
+    n1[n2[n1] != np.arange(len(n1))] = -1
+    return n1

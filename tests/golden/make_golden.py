@@ -302,7 +302,39 @@ def gen_whiten():
                         Y32=Y32, m32=m.astype(np.float32), P32=P.astype(np.float32))
 
 
+# ----------------------------------------------------------------------------- G7
+def gen_local():
+    """localHead (config 5 head, local_head.py:19-71) on a random NCHW map and
+    keypoints, reference module run unmodified."""
+    from cirtorch.modules.heads.local_head import localHead as R_localHead
+    r = data.rng(701)
+    out = {}
+    for tag, (b, c, h, w, n, e) in (("a", (2, 64, 13, 17, 50, 32)), ("b", (1, 128, 16, 24, 300, 128))):
+        x = r.standard_normal((b, c, h, w)).astype(np.float32)
+        kp = (r.random((b, n, 2)) * 2.2 - 1.1).astype(np.float32)   # some keypoints outside [-1, 1]
+        head = R_localHead(c, e)
+        sd = {"whiten.weight": (r.standard_normal((e, c)) * (1.0 / c) ** 0.5).astype(np.float32),
+              "whiten.bias": (r.standard_normal(e) * 0.05).astype(np.float32)}
+        head.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+        with torch.no_grad():
+            ref = head(torch.from_numpy(x), torch.from_numpy(kp)).numpy()
+        mine = ops.local_head(torch.from_numpy(x), torch.from_numpy(kp), torch.from_numpy(sd["whiten.weight"]),
+                              torch.from_numpy(sd["whiten.bias"])).numpy()
+        assert np.abs(ref - mine).max() < 1e-6, np.abs(ref - mine).max()
+        out.update({"x_" + tag: x, "kpts_" + tag: kp, "w_" + tag: sd["whiten.weight"], "b_" + tag: sd["whiten.bias"],
+                    "desc_" + tag: ref})
+    # mutual NN between two descriptor sets of set b (oracle restatement of HPatchesEval.nn_matcher)
+    d1 = out["desc_b"][0]
+    d2 = (d1[::-1] + 0.05 * r.standard_normal(d1.shape)).astype(np.float32)
+    d2 /= np.linalg.norm(d2, axis=1, keepdims=True)
+    out["nn_d2"] = d2
+    out["nn_match"] = ops.nn_matcher(d1, d2)
+    np.savez_compressed(os.path.join(HERE, "local.npz"), **out)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "local":
+        print("G7 local head"); gen_local(); sys.exit(0)
     print("G3 ops"); gen_ops()
     print("G1 resnet18@224"); gen_net("resnet18", (224, 224), 8, 1001, [(1,), (0.5, 1, 2)], "r18.npz",
                                       mixed=[(200, 240), (224, 192), (160, 160)])
@@ -312,4 +344,5 @@ if __name__ == "__main__":
     print("G4 knn"); gen_knn()
     print("G5 map"); gen_map()
     print("G6 whiten"); gen_whiten()
+    print("G7 local head"); gen_local()
     print("done")

@@ -125,3 +125,14 @@ def test_whiten_restatement():
     np.testing.assert_allclose(m, g["m"], rtol=1e-12)
     # eigenvectors are defined up to sign: compare |P| row-wise
     np.testing.assert_allclose(np.abs(P), np.abs(g["P"]), rtol=1e-6, atol=1e-8)
+
+
+def test_local_head_restatement():
+    """oracle.local_head == the reference localHead (local_head.py:43-71) on the G7 fixtures."""
+    import torch
+    g = golden("local.npz")
+    for tag in ("a", "b"):
+        got = ops.local_head(torch.from_numpy(g["x_" + tag]), torch.from_numpy(g["kpts_" + tag]),
+                             torch.from_numpy(g["w_" + tag]), torch.from_numpy(g["b_" + tag])).numpy()
+        np.testing.assert_allclose(got, g["desc_" + tag], rtol=0, atol=1e-6)
+    assert (ops.nn_matcher(g["desc_b"][0], g["nn_d2"]) == g["nn_match"]).all()
