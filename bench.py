@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=128, help="images (= queries) per rank per step")
-    ap.add_argument("--extract-batch", type=int, default=32,
+    ap.add_argument("--extract-batch", type=int, default=128,
                     help="images per extractor launch chain (the step's batch runs as batch/extract-batch chains)")
     ap.add_argument("--height", type=int, default=768)
     ap.add_argument("--width", type=int, default=1024)

@@ -112,3 +112,20 @@ def test_product_raises_on_cpu():
     from cirtorch.layers import functional as LF
     with pytest.raises(RuntimeError, match="GPU"):
         LF.gem(torch.rand(1, 4, 3, 3))
+
+
+def test_r50_batch128_chain_matches_small_chains(cuda):
+    """The bench's 128-image extractor chain (kernel variants and grids chosen
+    for that size, 32-bit buffer offsets near their limit) gives the same
+    descriptors as 4 chains of 32 images."""
+    from cirtorch.models.GF_net import make_net
+    from cirtorch.models.init import random_init_
+    net = make_net("resnet50", precision="bf16", mean=[0.485, 0.456, 0.406], std=[0.229, 0.224, 0.225])
+    random_init_(net, seed=0)
+    net = net.to(cuda).eval()
+    g = torch.Generator(device=cuda).manual_seed(5)
+    x = torch.rand((128, 3, 768, 1024), generator=g, device=cuda)
+    big = net.extract(x)
+    small = torch.cat([net.extract(x[i:i + 32]) for i in range(0, 128, 32)], dim=1)
+    cos = cosines(big.cpu().numpy(), small.cpu().numpy())
+    assert cos.min() > 1 - 1e-5, cos.min()

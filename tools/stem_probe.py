@@ -1,0 +1,32 @@
+"""Run the fused stem (rr_stem_conv_pool) repeatedly on a 32 x 3 x 768 x 1024
+batch, for rocprofv3 counter passes.  Developer tool."""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "image-retrieval-for-image-based-localization_amd"))
+sys.path.insert(0, REPO)
+import torch  # noqa: E402
+
+
+def main():
+    from cirtorch import _ops
+    x = torch.rand(32, 3, 768, 1024, device="cuda")
+    w = torch.randn(64, 3, 7, 7, device="cuda") * 0.1
+    wp = _ops.pack_stem_weights(w)
+    sc, sh = torch.rand(64, device="cuda") + 0.5, torch.randn(64, device="cuda") * 0.1
+    mean, std = [0.485, 0.456, 0.406], [0.229, 0.224, 0.225]
+    for _ in range(3):
+        _ops.stem_conv_pool(x, wp, sc, sh, mean=mean, std=std)
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(10):
+        _ops.stem_conv_pool(x, wp, sc, sh, mean=mean, std=std)
+    b.record()
+    torch.cuda.synchronize()
+    print("stem: %.1f us/launch" % (a.elapsed_time(b) * 100))
+
+
+if __name__ == "__main__":
+    main()
