@@ -37,12 +37,22 @@ struct StemArgs {
     const float* shift;
     bf16_t* y;        // [n][hp][wp][64]
     int n, h, w_, ho, wo, hp, wp;
-    float mean[3], stdv[3];
+    float mean[3], rstd[3];  // rstd = 1 / std (rounded once on the host)
     int do_norm, leaky;
     float slope;
 };
 
 constexpr int NT = 512;  // threads per block (8 waves)
+
+typedef __attribute__((ext_vector_type(2))) short short2v;
+
+// Two packed bf16 -> order-preserving int16 keys (and back: the map is an
+// involution): negative values get their magnitude bits flipped, so signed
+// 16-bit order == float order; max-pool then runs on v_pk_max_i16.
+__device__ __forceinline__ unsigned bf16_key2(unsigned w) {
+    const unsigned neg = (w >> 15) & 0x00010001u;
+    return w ^ (neg * 0x7FFFu);
+}
 
 template <int PH, int PW>
 __global__ void __launch_bounds__(NT) k_stem_pool(StemArgs a, int tiles_w, int tiles_hw, int ntiles) {
@@ -110,7 +120,7 @@ __global__ void __launch_bounds__(NT) k_stem_pool(StemArgs a, int tiles_w, int t
             float v[3];
 #pragma unroll
             for (int ch = 0; ch < 3; ++ch)  // zero padding is applied AFTER normalisation
-                v[ch] = (ok && a.do_norm) ? (pf[u][ch] - a.mean[ch]) / a.stdv[ch] : pf[u][ch];
+                v[ch] = (ok && a.do_norm) ? (pf[u][ch] - a.mean[ch]) * a.rstd[ch] : pf[u][ch];
             uint2 o;
             o.x = pack_bf16x2(v[0], v[1]);
             o.y = pack_bf16x2(v[2], 0.f);
@@ -158,18 +168,18 @@ __global__ void __launch_bounds__(NT) k_stem_pool(StemArgs a, int tiles_w, int t
                         v[r] = acc[2 * i2][r] * sS[cl + r] + sH[cl + r];
                         v[4 + r] = acc[2 * i2 + 1][r] * sS[cl + 4 + r] + sH[cl + 4 + r];
                     }
-                    if (a.leaky) {
+                    if (a.leaky) {  // slope in [0, 1] (host-checked): leaky(v) = max(v, slope * v)
 #pragma unroll
-                        for (int r = 0; r < 8; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * a.slope;
+                        for (int r = 0; r < 8; ++r) v[r] = fmaxf(v[r], v[r] * a.slope);
                     }
                     uint4 o;
                     if (valid) {
-                        o.x = pack_bf16x2(v[0], v[1]);
-                        o.y = pack_bf16x2(v[2], v[3]);
-                        o.z = pack_bf16x2(v[4], v[5]);
-                        o.w = pack_bf16x2(v[6], v[7]);
+                        o.x = bf16_key2(pack_bf16x2(v[0], v[1]));
+                        o.y = bf16_key2(pack_bf16x2(v[2], v[3]));
+                        o.z = bf16_key2(pack_bf16x2(v[4], v[5]));
+                        o.w = bf16_key2(pack_bf16x2(v[6], v[7]));
                     } else {
-                        o = make_uint4(0xFF80FF80u, 0xFF80FF80u, 0xFF80FF80u, 0xFF80FF80u);  // -inf: pool padding
+                        o = make_uint4(0x807F807Fu, 0x807F807Fu, 0x807F807Fu, 0x807F807Fu);  // key(-inf): pool padding
                     }
                     const int chunk = 4 * i2 + q;
                     *reinterpret_cast<uint4*>(sO + n * 128 + ((chunk ^ (n & 7)) << 4)) = o;
@@ -186,27 +196,27 @@ __global__ void __launch_bounds__(NT) k_stem_pool(StemArgs a, int tiles_w, int t
             const int c = item & 7, pp = item >> 3;
             const int pr = pp / PW, pc = pp - pr * PW;
             if (ph0 + pr >= a.hp || pw0 + pc >= a.wp) continue;
-            float mx[8];
+            // max over the 9 taps on order-preserving int16 keys of the bf16 values,
+            // two channels per v_pk_max_i16
+            short2v mx[4];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) mx[j] = -__builtin_inff();
+            for (int j = 0; j < 4; ++j) mx[j] = (short2v){(short)0x807F, (short)0x807F};
 #pragma unroll
             for (int dr = 0; dr < 3; ++dr)
 #pragma unroll
                 for (int dc = 0; dc < 3; ++dc) {
                     const int n = (2 * pr + dr) * SC + 2 * pc + dc;
                     const uint4 v = *reinterpret_cast<const uint4*>(sO + n * 128 + ((c ^ (n & 7)) << 4));
-                    const unsigned w4[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        mx[2 * j] = fmaxf(mx[2 * j], __uint_as_float(w4[j] << 16));
-                        mx[2 * j + 1] = fmaxf(mx[2 * j + 1], __uint_as_float(w4[j] & 0xffff0000u));
-                    }
+                    mx[0] = __builtin_elementwise_max(mx[0], __builtin_bit_cast(short2v, v.x));
+                    mx[1] = __builtin_elementwise_max(mx[1], __builtin_bit_cast(short2v, v.y));
+                    mx[2] = __builtin_elementwise_max(mx[2], __builtin_bit_cast(short2v, v.z));
+                    mx[3] = __builtin_elementwise_max(mx[3], __builtin_bit_cast(short2v, v.w));
                 }
             uint4 o;
-            o.x = pack_bf16x2(mx[0], mx[1]);
-            o.y = pack_bf16x2(mx[2], mx[3]);
-            o.z = pack_bf16x2(mx[4], mx[5]);
-            o.w = pack_bf16x2(mx[6], mx[7]);
+            o.x = bf16_key2(__builtin_bit_cast(unsigned, mx[0]));
+            o.y = bf16_key2(__builtin_bit_cast(unsigned, mx[1]));
+            o.z = bf16_key2(__builtin_bit_cast(unsigned, mx[2]));
+            o.w = bf16_key2(__builtin_bit_cast(unsigned, mx[3]));
             *reinterpret_cast<uint4*>(a.y + (((long long)img * a.hp + ph0 + pr) * a.wp + pw0 + pc) * 64 + 8 * c) = o;
         }
         __syncthreads();
@@ -261,9 +271,10 @@ extern "C" int rr_stem_conv_pool(const float* x, int n, int h, int w, const floa
     a.do_norm = do_normalize ? 1 : 0;
     for (int c = 0; c < 3; ++c) {
         a.mean[c] = do_normalize ? mean_host[c] : 0.f;
-        a.stdv[c] = do_normalize ? std_host[c] : 1.f;
+        a.rstd[c] = do_normalize ? (float)(1.0 / (double)std_host[c]) : 1.f;
     }
     a.leaky = act == RR_ACT_LEAKY;
+    if (a.leaky && !(slope >= 0.f && slope <= 1.f)) return fail(RR_EINVAL, "rr_stem_conv_pool: leaky slope must be in [0, 1]");
     a.slope = slope;
     constexpr int PH = 4, PW = 32;
     const int tiles_w = (wp + PW - 1) / PW, tiles_h = (hp + PH - 1) / PH;
