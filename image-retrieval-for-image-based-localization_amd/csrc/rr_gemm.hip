@@ -588,6 +588,8 @@ void launch_gemm2(const ConvArgs& a, bool k1, hipStream_t s) {
         launch_ns<T, TO, 256, 64, 4, 1, 2, 1>(a, k1, perm, s);
     else if (resid && a.kp < 512)
         launch_cfg3<T, TO, 256, 128, 4, 2>(a, k1, perm, s);
+    else if (resid && a.cout >= 2048 && a.P >= 65536)  // mod5 conv3 at >= 64 images: 256x64 tiles, -13 % (tune_layers)
+        launch_cfg3<T, TO, 256, 64, 4, 1>(a, k1, perm, s);
     else
         launch_cfg3<T, TO, 256, 256, 4, 2>(a, k1, perm, s);
 }
