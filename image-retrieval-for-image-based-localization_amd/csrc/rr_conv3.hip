@@ -339,7 +339,8 @@ void launch_c3(const ConvArgs& a, hipStream_t s) {
 }  // namespace
 
 int g_conv3_mode = 1;  // rr_set_tuning(RR_TUNE_CONV3X3): 0 off, 1 auto, 2 / 3 prefer 8x32 / 4x32 tiles,
-                       // 4 / 6 A-stationary with 1x8 / 1x4 waves (auto: 2x4), 7 3-stage weight ring
+                       // 4 / 6 A-stationary with 1x8 / 1x4 waves (auto: 2x4), 7 3-stage weight ring,
+                       // 8 256-channel x 6x32 tiles (auto where c_out % 256 == 0 and h % 6 == 0)
 
 // bf16 3x3 / stride 1 / pad 1 with PERM32 weights, bf16 out, no residual, and
 // image sizes the tiles divide; returns false otherwise (caller falls back to
@@ -364,6 +365,13 @@ bool launch_conv3x3(const ConvArgs& a, hipStream_t s) {
         // (tuning modes 2 / 3 force one of them where the image height allows)
         const long long t8 = a.h % 8 == 0 ? (long long)a.n * (a.h / 8) * (a.w_ / 32) * (a.cout / 128) : 0;
         const bool want8 = g_conv3_mode == 2 || (g_conv3_mode != 3 && t8 >= 2 * g_c3_cus);
+        // 256-channel tiles x 6 x 32 pixels (half the patch re-reads across channel
+        // tiles, 48 MFMAs per wave between barriers) for c_out % 256 == 0
+        // (measured at 128 x R50: mod4 c2 505 -> 461 us, mod5 c2 472 -> 416 us; default where it applies)
+        if ((g_conv3_mode == 1 || g_conv3_mode == 8) && a.cout % 256 == 0 && a.h % 6 == 0) {
+            launch_c3<256, 6, 32, 4, 2, false>(a, s);
+            return true;
+        }
         const bool deep = g_conv3_mode == 7;  // 3-stage weight ring
         if (t8 > 0 && (want8 || a.h % 4 != 0)) {
             if (deep) launch_c3<128, 8, 32, 2, 4, false, 3>(a, s);

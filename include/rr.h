@@ -216,7 +216,7 @@ int rr_mutual_nn(const long long* nn12, int n1, const long long* nn21, int n2, l
  *                        halo patches for the bf16 stride-1 3x3 convs;
  *                        2 / 3 prefer its 8x32 / 4x32 pixel tiles, 4 / 6 use
  *                        1x8 / 1x4 waves for the c_in = 64 A-stationary form,
- *                        7 a 3-stage weight ring
+ *                        7 a 3-stage weight ring, 8 256-channel x 6x32 tiles
  *   RR_TUNE_GRID_CUS     cap on the CUs one persistent launch spreads over
  *                        (0 = all; e.g. half the chip for two concurrent streams) */
 enum rr_tune_key { RR_TUNE_GEMM_CONFIG = 0, RR_TUNE_GEMM_STAGES = 1, RR_TUNE_GEMM_WIDE = 2,

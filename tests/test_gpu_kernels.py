@@ -94,11 +94,12 @@ CONV3_CASES = [
     (1, 128, 16, 64, 128, 3, 1, 1, False, True),   # two chunks
     (1, 256, 8, 32, 256, 3, 1, 1, False, True),    # two channel tiles
     (1, 512, 12, 32, 512, 3, 1, 1, False, True),   # 8 chunks, height only 4-divisible
+    (2, 256, 12, 64, 256, 3, 1, 1, False, True),   # 256-channel tiles (mode 8)
 ]
 
 
 @pytest.mark.parametrize("case", CONV3_CASES)
-@pytest.mark.parametrize("mode", [1, 2, 3, 4, 6, 7, 0])
+@pytest.mark.parametrize("mode", [1, 2, 3, 4, 6, 7, 8, 0])
 def test_conv3x3_direct(cuda, case, mode):
     """Direct 3x3 kernel (modes 1-4, 6: auto / 8x32 / 4x32 tiles / A-stationary wave layouts) and the
     implicit-GEMM fallback (mode 0) against the float64 reference."""
