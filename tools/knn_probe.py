@@ -1,0 +1,36 @@
+"""Time one search of Q queries (default 128, the bench step) against an N x 2048
+database (default 1M) for rocprofv3 kernel traces.  Developer tool."""
+import argparse
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "image-retrieval-for-image-based-localization_amd"))
+sys.path.insert(0, REPO)
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--q", type=int, default=128)
+    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--reps", type=int, default=10)
+    args = ap.parse_args()
+    from cirtorch import _ops
+    from cirtorch.search import KnnIndex
+    db = _ops.fill_unit_rows(args.n, 2048, seed=0xDB5EED)
+    q = _ops.fill_unit_rows(args.q, 2048, seed=0x0E5EED)
+    idx = KnnIndex(db, "bf16")
+    idx.search(q, 100)
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(args.reps):
+        idx.search(q, 100)
+    b.record()
+    torch.cuda.synchronize()
+    print("search Q=%d N=%d: %.3f ms" % (args.q, args.n, a.elapsed_time(b) / args.reps))
+
+
+if __name__ == "__main__":
+    main()
