@@ -10,10 +10,11 @@
 //  2. chunk select per (query, chunk): radix-select of the top KC fp32 keys
 //                  over L scores staged in LDS; candidates emitted in index
 //                  order (deterministic, ties -> lower index).
-//  3. final        per query: radix-select top KC of all chunk candidates,
+//  3. final        per query: radix-select top KC of all chunk candidates;
 //                  re-score them in float64 from the float32 rows (exact
-//                  products, fixed-order reduction), bitonic sort by
-//                  (score desc, index asc), emit k.
+//                  products, fixed-order reduction; one wave per candidate
+//                  over the whole chip); bitonic sort by (score desc,
+//                  index asc), emit k.
 // KC > k is the screening margin: bf16 scores err by ~1e-4, exact-f32 by
 // ~1e-7, far below KC-k candidates' worth of score density at the boundary.
 #include "rr_internal.h"
@@ -26,6 +27,7 @@ constexpr int SEL_WAVES = SEL_THREADS / 64;
 constexpr int CHUNK_L = 16384;           // rows per select chunk (keys staged in 64 KiB LDS)
 constexpr size_t SLAB_BUDGET = 64ull << 20;
 constexpr int MAX_SORT = 8192;
+constexpr int TOPK_BINS = 2048;          // radix-select histogram (11-bit digits)
 
 __device__ __forceinline__ uint32_t fkey(float f) {
     uint32_t u = __float_as_uint(f);
@@ -69,50 +71,60 @@ __device__ __forceinline__ int block_excl_scan(int v, int* wsum, int& total) {
 // in ascending position order; missing slots get (key 0, index -1).
 template <typename GK, typename GI>
 __device__ void block_topk(GK getk, GI geti, int len, int K, uint32_t* out_k, int* out_i, int* smem_i) {
-    int* hist = smem_i;             // 256
-    int* wsum = smem_i + 256;       // SEL_WAVES + 1
-    int* sel = smem_i + 256 + 32;   // [0]=digit, [1]=remaining
+    int* hist = smem_i;                        // TOPK_BINS
+    int* wsum = smem_i + TOPK_BINS;            // SEL_WAVES + 1
+    int* sel = smem_i + TOPK_BINS + 32;        // [0]=digit, [1]=remaining
     const int tid = threadIdx.x;
     uint32_t thr = 0;
     int remaining = K;
     if (len > K) {
+        // digits of 11, 11 and 10 bits: the first covers sign, exponent and two
+        // mantissa bits, so the scores' few exponents spread over many bins
+        // (fewer same-address LDS atomics than an 8-bit top digit), 3 passes.
         uint32_t prefix = 0, mask = 0;
-        for (int shift = 24; shift >= 0; shift -= 8) {
-            for (int i = tid; i < 256; i += SEL_THREADS) hist[i] = 0;
+        for (int pass = 0; pass < 3; ++pass) {
+            const int shift = pass == 0 ? 21 : pass == 1 ? 10 : 0;
+            const int bits = pass == 2 ? 10 : 11;
+            const uint32_t dmask = (1u << bits) - 1;
+            for (int i = tid; i < TOPK_BINS; i += SEL_THREADS) hist[i] = 0;
             __syncthreads();
             for (int i = tid; i < len; i += SEL_THREADS) {
                 uint32_t k = getk(i);
-                if ((k & mask) == prefix) atomicAdd(&hist[(k >> shift) & 255], 1);
+                if ((k & mask) == prefix) atomicAdd(&hist[(k >> shift) & dmask], 1);
             }
             __syncthreads();
             if (tid < 64) {
-                // wave 0: suffix sums over 256 bins (4 per lane), find the digit
-                int c0 = hist[tid * 4 + 0], c1 = hist[tid * 4 + 1], c2 = hist[tid * 4 + 2], c3 = hist[tid * 4 + 3];
-                int lsum = c0 + c1 + c2 + c3;
-                // inclusive suffix scan across lanes (lane 63 holds the highest digits)
-                int s = lsum;
+                // wave 0: lane owns bins [32*tid, 32*tid + 32); suffix sums
+                // across lanes (lane 63 holds the highest digits), then a walk
+                // down its own bins to the digit holding the K-th key
+                constexpr int PER = TOPK_BINS / 64;
+                int lsum = 0;
+#pragma unroll
+                for (int e = 0; e < PER; ++e) lsum += hist[tid * PER + e];
+                int sfx = lsum;
 #pragma unroll
                 for (int o = 1; o < 64; o <<= 1) {
-                    int y = __shfl_down(s, o, 64);
-                    if (tid + o < 64) s += y;
+                    int y = __shfl_down(sfx, o, 64);
+                    if (tid + o < 64) sfx += y;
                 }
-                int above = s - lsum;  // count of keys with digit > 4*tid+3
-                // within lane: digits 4*tid+3 .. 4*tid
-                int cs[4] = {c0, c1, c2, c3};
-                int acc = above;
-                for (int d = 3; d >= 0; --d) {
-                    if (acc < remaining && acc + cs[d] >= remaining) {
-                        sel[0] = tid * 4 + d;
-                        sel[1] = remaining - acc;
+                int acc = sfx - lsum;  // count of keys with digit above this lane's bins
+                if (acc < remaining && acc + lsum >= remaining) {
+                    for (int e = PER - 1; e >= 0; --e) {
+                        const int c = hist[tid * PER + e];
+                        if (acc + c >= remaining) {
+                            sel[0] = tid * PER + e;
+                            sel[1] = remaining - acc;
+                            break;
+                        }
+                        acc += c;
                     }
-                    acc += cs[d];
                 }
             }
             __syncthreads();
             const int digit = sel[0];
             remaining = sel[1];
             prefix |= (uint32_t)digit << shift;
-            mask |= 255u << shift;
+            mask |= dmask << shift;
             __syncthreads();
         }
         thr = prefix;
@@ -175,7 +187,7 @@ __global__ void __launch_bounds__(SEL_THREADS) k_chunk_select(const float* __res
                                                               int KC, uint32_t* __restrict__ cand_k,
                                                               int* __restrict__ cand_i) {
     extern __shared__ __attribute__((aligned(16))) uint32_t keys[];  // L
-    __shared__ int smi[256 + 64];
+    __shared__ int smi[TOPK_BINS + 64];
     const int q = blockIdx.x, c = blockIdx.y;
     const int len = min(L, rows_in_pass - c * L);
     const float* src = slab + (long long)q * S + (long long)c * L;
@@ -215,40 +227,68 @@ __device__ void bitonic_best_first(double* ks, I* is, int n) {
 }
 
 // ------------------------------------------------------------------ final
-// grid (nq).  Dynamic LDS: double ks[npow2] | int is[npow2] | u32 sk[KC] | int si[KC].
-__global__ void __launch_bounds__(SEL_THREADS) k_final(const uint32_t* __restrict__ cand_k, const int* __restrict__ cand_i,
-                                                       int ncand, int KC, int npow2, const float* __restrict__ db32,
-                                                       const float* __restrict__ q32, int d, int k,
-                                                       long long idx_offset, double* __restrict__ out_s,
-                                                       long long* __restrict__ out_i) {
-    extern __shared__ __attribute__((aligned(16))) char dyn[];
-    double* ks = reinterpret_cast<double*>(dyn);
-    int* is = reinterpret_cast<int*>(ks + npow2);
-    uint32_t* sk = reinterpret_cast<uint32_t*>(is + npow2);
-    int* si = reinterpret_cast<int*>(sk + KC);
-    __shared__ int smi[256 + 64];
+// Three launches per query batch, so the re-score runs on the whole chip:
+//  k_final_select  grid (nq):          top KC of the chunk candidates -> sel_i[q][KC]
+//  k_rescore       grid (npow2/4, nq): one wave per candidate, float64 score
+//  k_final_sort    grid (nq):          bitonic (score desc, index asc), emit k
+__global__ void __launch_bounds__(SEL_THREADS) k_final_select(const uint32_t* __restrict__ cand_k,
+                                                              const int* __restrict__ cand_i, int ncand, int KC,
+                                                              uint32_t* __restrict__ sel_k, int* __restrict__ sel_i) {
+    __shared__ int smi[TOPK_BINS + 64];
     const int q = blockIdx.x;
     const uint32_t* ck = cand_k + (long long)q * ncand;
     const int* ci = cand_i + (long long)q * ncand;
     // sentinel candidates (index -1) carry key 0 = below every real score key
-    block_topk([&](int i) { return ck[i]; }, [&](int i) { return ci[i]; }, ncand, KC, sk, si, smi);
-    // float64 re-score: one wave per candidate, lane-strided products in a
-    // fixed order, butterfly reduction -> bit-reproducible on any sharding.
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const float* qr = q32 + (long long)q * d;
-    for (int j = w; j < npow2; j += SEL_WAVES) {
-        const int idx = j < KC ? si[j] : -1;
-        double sc = -INFINITY;
-        if (idx >= 0) {
-            const float* dr = db32 + (long long)idx * d;
-            double acc = 0.0;
+    block_topk([&](int i) { return ck[i]; }, [&](int i) { return ci[i]; }, ncand, KC, sel_k + (long long)q * KC,
+               sel_i + (long long)q * KC, smi);
+}
+
+// float64 re-score from the float32 rows: exact products, a fixed per-lane
+// order and a butterfly reduction -> bit-reproducible on any sharding.
+__global__ void __launch_bounds__(256) k_rescore(const int* __restrict__ sel_i, int KC, int npow2,
+                                                 const float* __restrict__ db32, const float* __restrict__ q32, int d,
+                                                 double* __restrict__ fin_s, int* __restrict__ fin_i) {
+    const int q = blockIdx.y, lane = threadIdx.x & 63;
+    const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (j >= npow2) return;
+    const int idx = j < KC ? sel_i[(long long)q * KC + j] : -1;
+    double sc = -INFINITY;
+    if (idx >= 0) {
+        const float* dr = db32 + (long long)idx * d;
+        const float* qr = q32 + (long long)q * d;
+        double acc = 0.0;
+        if (d % 256 == 0) {
+#pragma unroll 4
+            for (int t = lane * 4; t < d; t += 256) {
+                const float4 x = *reinterpret_cast<const float4*>(dr + t);
+                const float4 y = *reinterpret_cast<const float4*>(qr + t);
+                acc = fma((double)x.x, (double)y.x, acc);
+                acc = fma((double)x.y, (double)y.y, acc);
+                acc = fma((double)x.z, (double)y.z, acc);
+                acc = fma((double)x.w, (double)y.w, acc);
+            }
+        } else {
             for (int t = lane; t < d; t += 64) acc = fma((double)dr[t], (double)qr[t], acc);
-            sc = wave_sum_d(acc);
         }
-        if (lane == 0) {
-            ks[j] = sc;
-            is[j] = idx >= 0 ? idx : 0x7fffffff;
-        }
+        sc = wave_sum_d(acc);
+    }
+    if (lane == 0) {
+        fin_s[(long long)q * npow2 + j] = sc;
+        fin_i[(long long)q * npow2 + j] = idx >= 0 ? idx : 0x7fffffff;
+    }
+}
+
+__global__ void __launch_bounds__(SEL_THREADS) k_final_sort(const double* __restrict__ fin_s,
+                                                            const int* __restrict__ fin_i, int npow2, int k,
+                                                            long long idx_offset, double* __restrict__ out_s,
+                                                            long long* __restrict__ out_i) {
+    extern __shared__ __attribute__((aligned(16))) char dyn[];
+    double* ks = reinterpret_cast<double*>(dyn);
+    int* is = reinterpret_cast<int*>(ks + npow2);
+    const int q = blockIdx.x;
+    for (int j = threadIdx.x; j < npow2; j += SEL_THREADS) {
+        ks[j] = fin_s[(long long)q * npow2 + j];
+        is[j] = fin_i[(long long)q * npow2 + j];
     }
     __syncthreads();
     bitonic_best_first(ks, is, npow2);
@@ -297,7 +337,7 @@ static int pow2_at_least(int v) {
 struct KnnPlan {
     int L, nchunks, G, KC, npow2;
     long long S;
-    size_t slab_bytes, cand_bytes, total;
+    size_t slab_bytes, cand_bytes, sel_bytes, fin_bytes, total;
 };
 
 static int default_cand(int k, int dtype) {
@@ -320,7 +360,9 @@ static KnnPlan plan(long long n_db, int nq, int k, int cand, int dtype) {
     p.npow2 = pow2_at_least(p.KC);
     p.slab_bytes = ((size_t)nq * p.S * 4 + 255) / 256 * 256;
     p.cand_bytes = (size_t)nq * p.nchunks * p.KC * 4;
-    p.total = p.slab_bytes + 2 * ((p.cand_bytes + 255) / 256 * 256);
+    p.sel_bytes = ((size_t)nq * p.KC * 4 + 255) / 256 * 256;
+    p.fin_bytes = ((size_t)nq * p.npow2 * 8 + 255) / 256 * 256 + ((size_t)nq * p.npow2 * 4 + 255) / 256 * 256;
+    p.total = p.slab_bytes + 2 * ((p.cand_bytes + 255) / 256 * 256) + 2 * p.sel_bytes + p.fin_bytes;
     return p;
 }
 
@@ -352,11 +394,16 @@ int rr_knn_topk(const void* db, const float* db_f32, long long n_db, const void*
     float* slab = (float*)ws;
     uint32_t* cand_k = (uint32_t*)(ws + p.slab_bytes);
     int* cand_i = (int*)(ws + p.slab_bytes + (p.cand_bytes + 255) / 256 * 256);
+    char* fws = ws + p.slab_bytes + 2 * ((p.cand_bytes + 255) / 256 * 256);
+    uint32_t* sel_k = (uint32_t*)fws;
+    int* sel_i = (int*)(fws + p.sel_bytes);
+    double* fin_s = (double*)(fws + 2 * p.sel_bytes);
+    int* fin_i = (int*)(fws + 2 * p.sel_bytes + ((size_t)nq * p.npow2 * 8 + 255) / 256 * 256);
 
     static bool attr_done = false;
     if (!attr_done) {
         (void)hipFuncSetAttribute((const void*)k_chunk_select, hipFuncAttributeMaxDynamicSharedMemorySize, CHUNK_L * 4);
-        (void)hipFuncSetAttribute((const void*)k_final, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 4096);
+        (void)hipFuncSetAttribute((const void*)k_final_sort, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 4096);
         (void)hipFuncSetAttribute((const void*)k_merge, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 4096);
         attr_done = true;
     }
@@ -378,10 +425,14 @@ int rr_knn_topk(const void* db, const float* db_f32, long long n_db, const void*
         hipLaunchKernelGGL(k_chunk_select, dim3(nq, chunks), dim3(SEL_THREADS), (size_t)p.L * 4, s, slab, p.S, p.L,
                            rows, (int)r0, (int)(r0 / p.L), p.nchunks, p.KC, cand_k, cand_i);
     }
-    const size_t fin_lds = (size_t)p.npow2 * 12 + (size_t)p.KC * 8;
+    const size_t fin_lds = (size_t)p.npow2 * 12;
     if (fin_lds > 160 * 1024 - 4096) return fail(RR_EINVAL, "rr_knn_topk: candidate set exceeds LDS");
-    hipLaunchKernelGGL(k_final, dim3(nq), dim3(SEL_THREADS), fin_lds, s, cand_k, cand_i, p.nchunks * p.KC, p.KC,
-                       p.npow2, db_f32, q_f32, d, k, idx_offset, out_scores, out_idx);
+    hipLaunchKernelGGL(k_final_select, dim3(nq), dim3(SEL_THREADS), 0, s, cand_k, cand_i, p.nchunks * p.KC, p.KC,
+                       sel_k, sel_i);
+    hipLaunchKernelGGL(k_rescore, dim3((p.npow2 + 3) / 4, nq), dim3(256), 0, s, sel_i, p.KC, p.npow2, db_f32, q_f32, d,
+                       fin_s, fin_i);
+    hipLaunchKernelGGL(k_final_sort, dim3(nq), dim3(SEL_THREADS), fin_lds, s, fin_s, fin_i, p.npow2, k, idx_offset,
+                       out_scores, out_idx);
     return check_launch("rr_knn_topk");
 }
 
