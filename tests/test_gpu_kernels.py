@@ -71,6 +71,8 @@ STREAM_CASES = [
     (1, 512, 63, 67, 128, 1, 1, 0, False, True),
     (1, 256, 65, 67, 1024, 1, 1, 0, True, True),
     (2, 256, 83, 101, 512, 1, 2, 0, False, False),   # strided projection
+    (1, 512, 64, 67, 2048, 1, 1, 0, True, True),     # mod5 conv3: 16 slices of 128 channels
+    (1, 512, 65, 67, 256, 1, 1, 0, False, True),     # mod4 conv1: 2 slices of 128 channels
 ]
 
 
