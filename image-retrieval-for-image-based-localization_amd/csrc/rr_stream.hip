@@ -461,9 +461,12 @@ bool launch_stream1x1(const ConvArgs& a, hipStream_t s) {
     // 128-channel slices of a 512-deep panel: the input is re-read per slice
     // (from L2 / Infinity Cache: slices of one strip run side by side), the
     // output and residual stream once (mod5 conv3 461 -> 600, mod4 conv1
-    // 606 -> 673 TFLOP/s at 128 images vs the tiled engine)
+    // 606 -> 673, mod4 projection 632 -> 695 TFLOP/s at 128 images vs the
+    // tiled engine).  K = 1024 does not fit: one strip's B operand alone is
+    // 128 VGPRs, and a single-strip-deep stream measured 395-410 vs 712-720.
     if (K == 512 && C == 2048 && res) { launch_s<128, 512, 1, 2, 8>(a, s); return true; }
     if (K == 512 && C == 256 && !res) { launch_s<128, 512, 1, 2, 8>(a, s); return true; }
+    if (K == 512 && C == 1024 && !res) { launch_s<128, 512, 1, 2, 8>(a, s); return true; }
     return false;
 }
 

@@ -73,6 +73,7 @@ STREAM_CASES = [
     (2, 256, 83, 101, 512, 1, 2, 0, False, False),   # strided projection
     (1, 512, 64, 67, 2048, 1, 1, 0, True, True),     # mod5 conv3: 16 slices of 128 channels
     (1, 512, 65, 67, 256, 1, 1, 0, False, True),     # mod4 conv1: 2 slices of 128 channels
+    (2, 512, 130, 70, 1024, 1, 2, 0, False, True),   # mod4 projection (stride 2): 8 slices
 ]
 
 
