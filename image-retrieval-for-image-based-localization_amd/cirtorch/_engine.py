@@ -17,13 +17,13 @@ import torch
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("RR_LIB", os.path.join(PKG_DIR, "librr.so"))
 
-RR_F32, RR_BF16 = 0, 1
+RR_F32, RR_BF16, RR_F16 = 0, 1, 2
 RR_ACT_IDENTITY, RR_ACT_LEAKY = 0, 1
 RR_POOL_GEM, RR_POOL_MAC, RR_POOL_SPOC = 0, 1, 2
 RR_CONV_AFFINE, RR_CONV_RESIDUAL, RR_CONV_PERM32 = 1, 2, 4
 RR_NHWC, RR_NCHW = 0, 1
 
-_DTYPE_CODE = {torch.float32: RR_F32, torch.bfloat16: RR_BF16}
+_DTYPE_CODE = {torch.float32: RR_F32, torch.bfloat16: RR_BF16, torch.float16: RR_F16}  # RR_F16: kNN screening only
 
 
 class ConvDesc(ctypes.Structure):
@@ -61,6 +61,7 @@ _SIGS = {
     "rr_set_tuning": ([_i, _i], _i),
     "rr_fill_unit_rows": ([_vp, _ll, _i, ctypes.c_ulonglong, _ll, _vp], _i),
     "rr_cast_f32_bf16": ([_vp, _vp, _ll, _vp], _i),
+    "rr_cast_f32_f16": ([_vp, _vp, _ll, _vp], _i),
 }
 
 _lib = None
@@ -112,7 +113,7 @@ def dtype_code(dt):
     try:
         return _DTYPE_CODE[dt]
     except KeyError:
-        raise RuntimeError("unsupported dtype %s (float32 or bfloat16)" % dt)
+        raise RuntimeError("unsupported dtype %s (float32, bfloat16; float16 for kNN screening)" % dt)
 
 
 def device_arch():

@@ -222,7 +222,7 @@ def knn_workspace_bytes(n_db, nq, d, k, cand=0, dtype=torch.float32):
 
 
 def knn_topk(db, db_f32, q, q_f32, k, cand=0, idx_offset=0, workspace=None):
-    """db/q: [n, D] rows in the screening dtype (float32 or bfloat16);
+    """db/q: [n, D] rows in the screening dtype (float32, bfloat16 or float16);
     db_f32/q_f32: the float32 rows used for the exact re-score.
     Returns (scores float64 [Q, k], idx int64 [Q, k])."""
     E.require_gpu(db, db_f32, q, q_f32)
@@ -266,6 +266,27 @@ def cast_bf16(x):
     y = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
     E.check(E.lib().rr_cast_f32_bf16(E.ptr(x), E.ptr(y), x.numel(), _st()), "rr_cast_f32_bf16")
     return y
+
+
+def cast_f16(x):
+    """float32 -> IEEE fp16 (round to nearest even): the kNN screening copy of an
+    fp16 database."""
+    E.require_gpu(x)
+    x = x.contiguous()
+    y = torch.empty(x.shape, dtype=torch.float16, device=x.device)
+    E.check(E.lib().rr_cast_f32_f16(E.ptr(x), E.ptr(y), x.numel(), _st()), "rr_cast_f32_f16")
+    return y
+
+
+def cast_screen(x, dtype):
+    """float32 rows -> the screening dtype's copy (the rows themselves for float32)."""
+    if dtype == torch.float32:
+        return x
+    if dtype == torch.bfloat16:
+        return cast_bf16(x)
+    if dtype == torch.float16:
+        return cast_f16(x)
+    raise RuntimeError("unsupported screening dtype %s" % dtype)
 
 
 # ---------------------------------------------------------------- local descriptors

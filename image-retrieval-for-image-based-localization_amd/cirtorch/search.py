@@ -6,7 +6,7 @@
   exactly ordered by (score desc, index asc); scores re-computed in float64.
 * ``rank(vecs, qvecs)``     -> full ranks (N x Q) for mAP evaluation (N <= 8192).
 * ``KnnIndex``              -> a resident database (float32 rows + optional
-  bf16 screening copy) queried many times.
+  bf16 or fp16 screening copy) queried many times.
 * ``ShardedIndex``          -> database rows split over the ranks of a
   torch.distributed group (RCCL on ROCm), per-shard top-k, all-gather of the
   (score, index) lists, on-GPU merge — bit-identical to the 1-GPU result.
@@ -21,7 +21,8 @@ import torch.distributed as dist
 
 from . import _ops
 
-_PREC = {"fp32": torch.float32, "float32": torch.float32, "bf16": torch.bfloat16, "bfloat16": torch.bfloat16}
+_PREC = {"fp32": torch.float32, "float32": torch.float32, "bf16": torch.bfloat16, "bfloat16": torch.bfloat16,
+         "fp16": torch.float16, "float16": torch.float16}
 
 
 def _rows(cols):
@@ -39,7 +40,7 @@ class KnnIndex:
         """db_rows: [N, D] float32 on the GPU (kept by reference, not copied)."""
         self.db32 = db_rows.float().contiguous()
         self.dtype = _PREC[precision]
-        self.db = self.db32 if self.dtype == torch.float32 else _ops.cast_bf16(self.db32)
+        self.db = _ops.cast_screen(self.db32, self.dtype)
         self.cand = cand
         self.idx_offset = idx_offset
         self._ws = None
@@ -50,7 +51,7 @@ class KnnIndex:
 
     def search(self, q_rows, k):
         q32 = q_rows.float().contiguous()
-        q = q32 if self.dtype == torch.float32 else _ops.cast_bf16(q32)
+        q = _ops.cast_screen(q32, self.dtype)
         need = _ops.knn_workspace_bytes(self.ntotal, q.shape[0], q.shape[1], k, self.cand, self.dtype)
         if self._ws is None or self._ws.numel() < need:
             self._ws = torch.empty(need, dtype=torch.uint8, device=q.device)

@@ -327,7 +327,7 @@ static bool use_v2(const ConvArgs& a, int dtype) {
         forced = (e && e[0] == '1') ? 1 : 0;
     }
     if (forced == 1) return false;
-    const int esz = dtype == RR_BF16 ? 2 : 4;
+    const int esz = dtype == RR_F32 ? 4 : 2;
     const long long xbytes = (long long)a.n * a.h * a.w_ * a.cin * esz;
     return (a.kp * esz) % 128 == 0 && xbytes < (1ll << 31) && (long long)256 * a.kp * esz < (1ll << 31);
 }
@@ -344,6 +344,7 @@ static void dispatch(const ConvArgs& a, bool k1, int dtype, hipStream_t s) {
 
 void gemm_scores(const ConvArgs& a, int dtype, hipStream_t s) {
     if (dtype == RR_BF16) dispatch<bf16_t, float>(a, true, dtype, s);
+    else if (dtype == RR_F16) launch_gemm2<f16_t, float>(a, true, s);  // LDS-DMA engine only (d >= 64: 128-B K-steps)
     else dispatch<float, float>(a, true, dtype, s);
 }
 

@@ -24,10 +24,12 @@
 namespace rr {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8_t;
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;
 
 template <typename T> struct Vec2;
 template <> struct Vec2<bf16_t> { static constexpr int N = 8; };
+template <> struct Vec2<f16_t> { static constexpr int N = 8; };
 template <> struct Vec2<float> { static constexpr int N = 4; };
 
 constexpr unsigned OOB = 0x80000000u;  // voffset beyond every buffer: reads as 0
@@ -442,7 +444,15 @@ __global__ void __launch_bounds__(64 * WC * WP, ((NS == 2 && AK * TC <= 256) || 
             for (int i = 0; i < FM; ++i) fa[i] = *reinterpret_cast<const uint4*>(As + swz(arow0 + i * 16, kq + 4 * hs));
 #pragma unroll
             for (int j = 0; j < FN; ++j) fb[j] = *reinterpret_cast<const uint4*>(Bs + swz(brow0 + j * 16, kq + 4 * hs));
-            if constexpr (VEC == 8) {
+            if constexpr (std::is_same<T, f16_t>::value) {
+#pragma unroll
+                for (int i = 0; i < FM; ++i)
+#pragma unroll
+                    for (int j = 0; j < FN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, fa[i]),
+                                                                           __builtin_bit_cast(f16x8_t, fb[j]),
+                                                                           acc[i][j], 0, 0, 0);
+            } else if constexpr (VEC == 8) {
 #pragma unroll
                 for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -605,6 +615,7 @@ void set_gemm_tuning(int key, int value) {
 
 template void launch_gemm2<bf16_t, bf16_t>(const ConvArgs&, bool, hipStream_t);
 template void launch_gemm2<bf16_t, float>(const ConvArgs&, bool, hipStream_t);
+template void launch_gemm2<f16_t, float>(const ConvArgs&, bool, hipStream_t);
 template void launch_gemm2<float, float>(const ConvArgs&, bool, hipStream_t);
 
 }  // namespace rr

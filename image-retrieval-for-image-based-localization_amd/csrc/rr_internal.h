@@ -30,6 +30,7 @@ inline int check_launch(const char* what) {
 
 // bf16 stored as raw uint16 bits.
 typedef uint16_t bf16_t;
+typedef _Float16 f16_t;  // IEEE binary16 (kNN screening copies)
 
 __device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 

@@ -341,7 +341,7 @@ struct KnnPlan {
 };
 
 static int default_cand(int k, int dtype) {
-    int extra = dtype == RR_BF16 ? 128 : 32;
+    int extra = dtype == RR_BF16 ? 128 : dtype == RR_F16 ? 64 : 32;  // screening error: bf16 ~1e-4, fp16 ~1e-5
     return ((k + extra + 63) / 64) * 64;
 }
 
@@ -383,7 +383,8 @@ int rr_knn_topk(const void* db, const float* db_f32, long long n_db, const void*
                 size_t workspace_bytes, int dtype, void* stream) {
     if (n_db <= 0 || nq <= 0 || k <= 0) return fail(RR_EINVAL, "rr_knn_topk: empty problem");
     if (n_db > 0x7fffffffll) return fail(RR_EINVAL, "rr_knn_topk: shard rows must fit int32 (shard the database)");
-    if (dtype != RR_BF16 && dtype != RR_F32) return fail(RR_EINVAL, "rr_knn_topk: dtype");
+    if (dtype != RR_BF16 && dtype != RR_F32 && dtype != RR_F16) return fail(RR_EINVAL, "rr_knn_topk: dtype");
+    if (dtype == RR_F16 && d < 64) return fail(RR_EINVAL, "rr_knn_topk: fp16 screening needs d >= 64");
     if (d <= 0 || d % 32 || (d & (d - 1))) return fail(RR_EINVAL, "rr_knn_topk: d must be a power of two >= 32");
     KnnPlan p = plan(n_db, nq, k, cand, dtype);
     if (p.KC < k) return fail(RR_EINVAL, "rr_knn_topk: cand must be >= k");
@@ -408,7 +409,7 @@ int rr_knn_topk(const void* db, const float* db_f32, long long n_db, const void*
         attr_done = true;
     }
 
-    const size_t esz = dtype == RR_BF16 ? 2 : 4;
+    const size_t esz = dtype == RR_F32 ? 4 : 2;
     for (long long r0 = 0; r0 < n_db; r0 += (long long)p.G * p.L) {
         const int rows = (int)((n_db - r0) < (long long)p.G * p.L ? (n_db - r0) : (long long)p.G * p.L);
         ConvArgs a{};

@@ -215,6 +215,16 @@ __global__ void __launch_bounds__(256) k_fill_unit_rows(float* __restrict__ out,
     }
 }
 
+__global__ void k_cast_f32_f16(const float* __restrict__ x, f16_t* __restrict__ y, long long n) {
+    const long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    if (i + 3 < n) {
+        const float4 v = *reinterpret_cast<const float4*>(x + i);
+        y[i] = (f16_t)v.x; y[i + 1] = (f16_t)v.y; y[i + 2] = (f16_t)v.z; y[i + 3] = (f16_t)v.w;
+    } else {
+        for (long long j = i; j < n; ++j) y[j] = (f16_t)x[j];
+    }
+}
+
 __global__ void k_cast_f32_bf16(const float* __restrict__ x, bf16_t* __restrict__ y, long long n) {
     long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
     if (i + 3 < n) {
@@ -309,6 +319,14 @@ int rr_fill_unit_rows(float* out, long long rows, int d, unsigned long long seed
                            (uint64_t)seed, row0 + r);
     }
     return check_launch("rr_fill_unit_rows");
+}
+
+int rr_cast_f32_f16(const float* x, void* y, long long n, void* stream) {
+    if (n <= 0) return RR_OK;
+    if (!x || !y) return fail(RR_EINVAL, "rr_cast_f32_f16: null pointer");
+    hipLaunchKernelGGL(k_cast_f32_f16, dim3(nblk((n + 3) / 4, 256)), dim3(256), 0, as_stream(stream), x,
+                       (f16_t*)y, n);
+    return check_launch("rr_cast_f32_f16");
 }
 
 int rr_cast_f32_bf16(const float* x, void* y, long long n, void* stream) {

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-enum rr_dtype { RR_F32 = 0, RR_BF16 = 1 };
+enum rr_dtype { RR_F32 = 0, RR_BF16 = 1, RR_F16 = 2 };  /* RR_F16: kNN screening only */
 enum rr_act { RR_ACT_IDENTITY = 0, RR_ACT_LEAKY = 1 };
 enum rr_pool_mode { RR_POOL_GEM = 0, RR_POOL_MAC = 1, RR_POOL_SPOC = 2 };
 enum rr_conv_flags { RR_CONV_AFFINE = 1, RR_CONV_RESIDUAL = 2, RR_CONV_PERM32 = 4 };
@@ -163,8 +163,9 @@ int rr_head_l2n_whiten_l2n(const float* x, int rows, int dim, const float* w, co
  * Replaces `scores = np.dot(vecs.T, qvecs); ranks = np.argsort(-scores, axis=0)`
  * (scripts/test.py:247-248, scripts/train_globalF.py:733-734), returning only
  * the first k ranks.  Candidates are screened with an MFMA score GEMM in
- * `dtype` (db/q), then re-scored in float64 from the float32 copies and
- * ordered by (score desc, index asc).
+ * `dtype` (db/q: RR_F32, RR_BF16, or RR_F16 — the fp16 database of SURVEY
+ * §8d config 5; d >= 64 for the 16-bit types), then re-scored in float64
+ * from the float32 copies and ordered by (score desc, index asc).
  *   db      : [n_db][d] (dtype)      db_f32 : [n_db][d] float32 (re-rank)
  *   q       : [nq][d]   (dtype)      q_f32  : [nq][d]   float32
  *   out_scores : [nq][k] float64     out_idx : [nq][k] int64 (+ idx_offset)
@@ -231,6 +232,8 @@ int rr_fill_unit_rows(float* out, long long rows, int d, unsigned long long seed
                       long long row0, void* stream);
 /* float32 -> bf16 (round to nearest even). */
 int rr_cast_f32_bf16(const float* x, void* y, long long n, void* stream);
+/* float32 -> fp16 (IEEE binary16, round to nearest even). */
+int rr_cast_f32_f16(const float* x, void* y, long long n, void* stream);
 
 #ifdef __cplusplus
 }

@@ -3,6 +3,8 @@
 the reference's, full ranks identical to np.argsort for mAP, shard merge
 bit-identical to the single-GPU result."""
 
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -12,7 +14,7 @@ from conftest import golden
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16", "fp16"])
 @pytest.mark.parametrize("tag", ["4k", "100k"])
 def test_knn_vs_reference_golden(cuda, precision, tag):
     from cirtorch.search import KnnIndex
@@ -34,7 +36,7 @@ def test_knn_matches_exact_oracle_random_shapes(cuda):
         qq = data.unit_rows(q, d, seed=n + 1)
         kk = min(k, n)
         ref_s, ref_i = ops.topk_exact(db, qq, kk)
-        for prec in ("fp32", "bf16"):
+        for prec in ("fp32", "bf16", "fp16"):
             s, i = KnnIndex(torch.from_numpy(db).to(cuda), prec).search(torch.from_numpy(qq).to(cuda), kk)
             np.testing.assert_array_equal(i.cpu().numpy(), ref_i, err_msg="%s %s" % (prec, (n, q, d, k)))
             np.testing.assert_allclose(s.cpu().numpy(), ref_s, rtol=0, atol=1e-12)
@@ -90,3 +92,23 @@ def test_topk_merge_equals_single_shard(cuda):
         ii.append(i)
     sm, im = merge_topk(torch.stack(ss), torch.stack(ii), k)
     assert torch.equal(im, i1) and torch.equal(sm, s1)
+
+
+def test_fp16_screening_copy_and_limits(cuda):
+    """The fp16 screening copy is IEEE binary16 round-to-nearest-even (== torch
+    .half()); fp16 screening needs d >= 64 and is rejected by the conv engine."""
+    from cirtorch import _ops
+    from cirtorch import _engine as E
+    from cirtorch.search import KnnIndex
+    from oracle import data
+    x = torch.randn(1003, 64, device=cuda) * 3.0
+    assert torch.equal(_ops.cast_f16(x), x.half())
+    db = torch.from_numpy(data.unit_rows(100, 32, seed=5)).to(cuda)
+    with pytest.raises(RuntimeError, match="d >= 64"):
+        KnnIndex(db, "fp16").search(db[:2], 3)
+    xh = torch.zeros(1, 4, 4, 64, dtype=torch.float16, device=cuda)
+    w = torch.zeros(64, 64, dtype=torch.float16, device=cuda)
+    y = torch.empty(16, 64, dtype=torch.float16, device=cuda)
+    d = E.ConvDesc(1, 4, 4, 64, 4, 4, 64, 1, 1, 1, 0, 1, 64, 64, 0, 0.0, 0)
+    rc = E.lib().rr_conv2d_fused(E.ptr(xh), E.ptr(w), None, None, None, E.ptr(y), ctypes.byref(d), 2, 2, None)
+    assert rc == -1 and b"dtype" in E.lib().rr_last_error()

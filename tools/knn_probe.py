@@ -15,8 +15,13 @@ def main():
     ap.add_argument("--q", type=int, default=128)
     ap.add_argument("--n", type=int, default=1_000_000)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--tune", default="", help="rr_set_tuning pairs key=value[,key=value]")
     args = ap.parse_args()
     from cirtorch import _ops
+    from cirtorch import _engine as E
+    for kv in filter(None, args.tune.split(",")):
+        k_, v_ = kv.split("=")
+        E.check(E.lib().rr_set_tuning(int(k_), int(v_)), "rr_set_tuning")
     from cirtorch.search import KnnIndex
     db = _ops.fill_unit_rows(args.n, 2048, seed=0xDB5EED)
     q = _ops.fill_unit_rows(args.q, 2048, seed=0x0E5EED)
@@ -29,7 +34,7 @@ def main():
         idx.search(q, 100)
     b.record()
     torch.cuda.synchronize()
-    print("search Q=%d N=%d: %.3f ms" % (args.q, args.n, a.elapsed_time(b) / args.reps))
+    print("search Q=%d N=%d tune=%s: %.3f ms" % (args.q, args.n, args.tune, a.elapsed_time(b) / args.reps))
 
 
 if __name__ == "__main__":
