@@ -58,6 +58,7 @@ def parse():
     ap.add_argument("--knn-steps", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--local-kpts", type=int, default=2048, help="keypoints per image for the local-head sub-benchmark (0 = skip)")
+    ap.add_argument("--latency", type=int, default=1, help="single-image extract latency, eager vs HIP-graph replay (0 = skip)")
     ap.add_argument("--overlap", action="store_true",
                     help="run batch i's match on a second stream, overlapping batch i+1's extract (measured slower on one GPU)")
     ap.add_argument("--cpu-images", type=int, default=2)
@@ -322,6 +323,29 @@ def main():
                  "note": "rr_local_head (bilinear sample + exact-f32 MFMA Linear + normalize) on a synthetic bf16 map; "
                          "mutual_nn = two exact top-1 searches (%d x %d x 128) + rr_mutual_nn"
                          % (args.local_kpts, args.local_kpts)}
+    # serving latency: one image through the extractor, eager launches vs one
+    # HIP-graph replay of the same launches (cirtorch.utils.graph)
+    latency = None
+    if args.latency and rank == 0:
+        from cirtorch.utils.graph import GraphedForward
+        x1 = images[:1].contiguous()
+        gf = GraphedForward(lambda t: net.extract(t), x1)
+        ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        res = {}
+        for name, fn in (("eager", lambda: net.extract(x1)), ("graph", lambda: gf(x1))):
+            for _ in range(3):
+                fn()
+            torch.cuda.synchronize()
+            ea.record()
+            for _ in range(20):
+                fn()
+            eb.record()
+            torch.cuda.synchronize()
+            res[name] = ea.elapsed_time(eb) / 20
+        latency = {"batch": 1, "eager_ms": res["eager"], "graph_ms": res["graph"],
+                   "note": "one 3x%dx%d image, extract (body + GeM/L2N/whiten/L2N); graph = torch.cuda.CUDAGraph "
+                           "(hipGraph) capture of the same librr launches, replayed" % (H, W)}
+        del gf
     fl_img = conv_flops_per_image(net.body, H, W)
     costs = layer_costs(net.body, H, W, 2 if args.precision == "bf16" else 4)
     peak_m = (PEAK_BF16_TFLOPS if args.precision == "bf16" else PEAK_F32_TFLOPS) * 1e12
@@ -365,6 +389,7 @@ def main():
         "extract_images_per_sec": ext_only * world,
         "knn": knn,
         "local": local,
+        "latency": latency,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args)
