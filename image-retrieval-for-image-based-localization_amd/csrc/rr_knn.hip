@@ -37,35 +37,6 @@ __device__ __forceinline__ float funkey(uint32_t k) {
     return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
 }
 
-// Block-wide exclusive scan of one int per thread (SEL_THREADS threads).
-__device__ __forceinline__ int block_excl_scan(int v, int* wsum, int& total) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    int x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        int y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) wsum[w] = x;
-    __syncthreads();
-    if (w == 0) {
-        int t = lane < SEL_WAVES ? wsum[lane] : 0;
-        int s = t;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            int y = __shfl_up(s, o, 64);
-            if (lane >= o) s += y;
-        }
-        if (lane < SEL_WAVES) wsum[lane] = s - t;
-        if (lane == SEL_WAVES - 1) wsum[SEL_WAVES] = s;
-    }
-    __syncthreads();
-    int res = wsum[w] + x - v;
-    total = wsum[SEL_WAVES];
-    __syncthreads();
-    return res;
-}
-
 // Top-K (largest keys) of keys[0..len) with index-order ties.  `getk(i)` gives
 // the key, `geti(i)` the payload index; K results are written to out_k/out_i
 // in ascending position order; missing slots get (key 0, index -1).
@@ -129,48 +100,54 @@ __device__ void block_topk(GK getk, GI geti, int len, int K, uint32_t* out_k, in
         }
         thr = prefix;
     }
-    // ordered emission: thread t owns the contiguous segment [t*seg, (t+1)*seg)
-    const int seg = (len + SEL_THREADS - 1) / SEL_THREADS;
-    const int b = tid * seg, e = min(len, b + seg);
-    int ngt = 0, neq = 0;
-    if (len > K) {
-        for (int i = b; i < e; ++i) {
-            uint32_t k = getk(i);
-            ngt += k > thr;
-            neq += k == thr;
-        }
-    } else {
-        ngt = max(0, e - b);
+    // ordered emission: wave w owns the contiguous range [wb, we) and walks it
+    // 64 keys at a time (stride-1 reads); ballot + mbcnt give each key's rank
+    // among the taken keys before it, one 16-entry scan orders the waves.
+    const int lane = tid & 63, w = tid >> 6;
+    int* wgt = wsum;                 // SEL_WAVES counts of keys above the threshold
+    int* weq = smem_i + TOPK_BINS + 40;  // SEL_WAVES counts of keys equal to it
+    const bool sel_all = len <= K;
+    const int wseg = (((len + SEL_WAVES - 1) / SEL_WAVES) + 63) & ~63;
+    const int wb = min(len, w * wseg), we = min(len, wb + wseg);
+    int cgt = 0, ceq = 0;
+    for (int i0 = wb; i0 < we; i0 += 64) {
+        const int i = i0 + lane;
+        const bool in = i < we;
+        const uint32_t k = in ? getk(i) : 0u;
+        cgt += __popcll(__ballot(in && (sel_all || k > thr)));
+        ceq += __popcll(__ballot(in && !sel_all && k == thr));
     }
-    int tot_gt, tot_eq;
-    int pgt = block_excl_scan(ngt, wsum, tot_gt);
-    int peq = block_excl_scan(neq, wsum, tot_eq);
-    // gt items occupy [0, tot_gt) in position order; then the first
-    // `remaining` eq items.  Merge both in position order: an item's slot is
-    // (#gt before it) + (#taken eq before it).
-    if (len > K) {
-        int gi = pgt, ei = peq;
-        for (int i = b; i < e; ++i) {
-            uint32_t k = getk(i);
-            if (k > thr) {
-                int slot = gi + min(ei, remaining);
-                out_k[slot] = k;
-                out_i[slot] = geti(i);
-                ++gi;
-            } else if (k == thr) {
-                if (ei < remaining) {
-                    int slot = gi + ei;
-                    out_k[slot] = k;
-                    out_i[slot] = geti(i);
-                }
-                ++ei;
-            }
+    if (lane == 0) {
+        wgt[w] = cgt;
+        weq[w] = ceq;
+    }
+    __syncthreads();
+    int pgt = 0, peq = 0;
+    for (int j = 0; j < w; ++j) {
+        pgt += wgt[j];
+        peq += weq[j];
+    }
+    for (int i0 = wb; i0 < we; i0 += 64) {
+        const int i = i0 + lane;
+        const bool in = i < we;
+        const uint32_t k = in ? getk(i) : 0u;
+        const bool gt = in && (sel_all || k > thr);
+        const bool eq = in && !sel_all && k == thr;
+        const unsigned long long bg = __ballot(gt), be = __ballot(eq);
+        const int rg = pgt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bg >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bg, 0u));
+        const int re = peq + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(be >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)be, 0u));
+        if (gt) {
+            const int slot = rg + min(re, remaining);
+            out_k[slot] = k;
+            out_i[slot] = geti(i);
+        } else if (eq && re < remaining) {
+            out_k[rg + re] = k;
+            out_i[rg + re] = geti(i);
         }
-    } else {
-        for (int i = b; i < e; ++i) {
-            out_k[pgt + i - b] = getk(i);
-            out_i[pgt + i - b] = geti(i);
-        }
+        pgt += __popcll(bg);
+        peq += __popcll(be);
+    }
+    if (sel_all) {
         for (int i = len + tid; i < K; i += SEL_THREADS) {
             out_k[i] = 0u;
             out_i[i] = -1;
@@ -191,7 +168,13 @@ __global__ void __launch_bounds__(SEL_THREADS) k_chunk_select(const float* __res
     const int q = blockIdx.x, c = blockIdx.y;
     const int len = min(L, rows_in_pass - c * L);
     const float* src = slab + (long long)q * S + (long long)c * L;
-    for (int i = threadIdx.x; i < len; i += SEL_THREADS) keys[i] = fkey(src[i]);
+    // slab rows start 16-B aligned (S % 4 == 0, L % 4 == 0): float4 loads
+    const int len4 = len & ~3;
+    for (int i = threadIdx.x * 4; i < len4; i += SEL_THREADS * 4) {
+        const float4 v = *reinterpret_cast<const float4*>(src + i);
+        *reinterpret_cast<uint4*>(keys + i) = make_uint4(fkey(v.x), fkey(v.y), fkey(v.z), fkey(v.w));
+    }
+    for (int i = len4 + threadIdx.x; i < len; i += SEL_THREADS) keys[i] = fkey(src[i]);
     __syncthreads();
     const long long o = ((long long)q * nchunks + chunk0 + c) * KC;
     const int base = row0 + c * L;
