@@ -71,7 +71,7 @@ __device__ void block_topk(GK getk, GI geti, int len, int K, uint32_t* out_k, in
                 constexpr int PER = TOPK_BINS / 64;
                 int lsum = 0;
 #pragma unroll
-                for (int e = 0; e < PER; ++e) lsum += hist[tid * PER + e];
+                for (int e = 0; e < PER; ++e) lsum += hist[tid * PER + ((e + tid) & (PER - 1))];  // rotated: conflict-free
                 int sfx = lsum;
 #pragma unroll
                 for (int o = 1; o < 64; o <<= 1) {
