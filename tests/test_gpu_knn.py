@@ -112,3 +112,46 @@ def test_fp16_screening_copy_and_limits(cuda):
     d = E.ConvDesc(1, 4, 4, 64, 4, 4, 64, 1, 1, 1, 0, 1, 64, 64, 0, 0.0, 0)
     rc = E.lib().rr_conv2d_fused(E.ptr(xh), E.ptr(w), None, None, None, E.ptr(y), ctypes.byref(d), 2, 2, None)
     assert rc == -1 and b"dtype" in E.lib().rr_last_error()
+
+
+def test_knn_full_size_1m_bench_shape(cuda):
+    """BASELINE config size (1M x 2048 database, 128 queries, k = 100, bf16
+    screening) through size-independent properties: a query that is a database
+    row retrieves itself first with score 1; two queries checked against the
+    CPU oracle over the whole database (chunked exact float64 top-k); a
+    4-shard search + merge is bit-identical to the single search."""
+    from cirtorch import _ops
+    from cirtorch.search import KnnIndex, merge_topk
+    from oracle import ops
+    n, d, q, k = 1_000_000, 2048, 128, 100
+    db = _ops.fill_unit_rows(n, d, seed=0xDB5EED, device=cuda)
+    qq = _ops.fill_unit_rows(q, d, seed=0x0E5EED, device=cuda)
+    self_rows = [5, 77777, 500000, n - 1]
+    qq[:4] = db[self_rows]
+    index = KnnIndex(db, "bf16")
+    s, i = index.search(qq, k)
+    i_np, s_np = i.cpu().numpy(), s.cpu().numpy()
+    assert i_np[:4, 0].tolist() == self_rows
+    assert np.abs(s_np[:4, 0] - 1.0).max() < 1e-6
+    assert (np.diff(s_np, axis=1) <= 0).all()                      # sorted best first
+    # exact oracle for two queries over all 1M rows (chunked)
+    db_np, q_np = db.cpu().numpy(), qq[4:6].cpu().numpy()
+    cs, ci = [], []
+    for r0 in range(0, n, 125_000):
+        s_c, i_c = ops.topk_exact(db_np[r0:r0 + 125_000], q_np, k)
+        cs.append(s_c)
+        ci.append(i_c + r0)
+    cs, ci = np.concatenate(cs, 1), np.concatenate(ci, 1)
+    for j in range(2):
+        order = np.lexsort((ci[j], -cs[j]))[:k]
+        np.testing.assert_array_equal(i_np[4 + j], ci[j][order])
+        np.testing.assert_allclose(s_np[4 + j], cs[j][order], rtol=0, atol=1e-12)
+    # 4 shards + merge == single
+    R, per = 4, n // 4
+    ss, ii = [], []
+    for r in range(R):
+        sh_s, sh_i = KnnIndex(db[r * per:(r + 1) * per], "bf16", idx_offset=r * per).search(qq, k)
+        ss.append(sh_s)
+        ii.append(sh_i)
+    sm, im = merge_topk(torch.stack(ss), torch.stack(ii), k)
+    assert torch.equal(im, i) and torch.equal(sm, s)
