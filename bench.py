@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--height", type=int, default=768)
     ap.add_argument("--width", type=int, default=1024)
     ap.add_argument("--arch", default="resnet50")
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp16", "fp32"])
     ap.add_argument("--db-rows", type=int, default=1_000_000)
     ap.add_argument("--dim", type=int, default=2048)
     ap.add_argument("--k", type=int, default=100)
@@ -274,7 +274,7 @@ def main():
                 dist.all_reduce(t, op=dist.ReduceOp.MAX)
                 tk = float(t.item())
             flops = 2.0 * args.knn_q * n_local * args.dim
-            peak = PEAK_BF16_TFLOPS if args.precision == "bf16" else PEAK_F32_TFLOPS
+            peak = PEAK_F32_TFLOPS if args.precision == "fp32" else PEAK_BF16_TFLOPS
             knn = {"queries_per_sec": args.knn_q / tk, "q": args.knn_q, "db_rows": args.db_rows, "k": args.k,
                    "ms_per_batch": tk * 1e3,
                    "roofline": {"bound": "mfma", "achieved": flops / tk / 1e12, "peak": peak, "unit": "TFLOP/s",
@@ -347,12 +347,12 @@ def main():
                            "(hipGraph) capture of the same librr launches, replayed" % (H, W)}
         del gf
     fl_img = conv_flops_per_image(net.body, H, W)
-    costs = layer_costs(net.body, H, W, 2 if args.precision == "bf16" else 4)
-    peak_m = (PEAK_BF16_TFLOPS if args.precision == "bf16" else PEAK_F32_TFLOPS) * 1e12
+    costs = layer_costs(net.body, H, W, 4 if args.precision == "fp32" else 2)
+    peak_m = (PEAK_F32_TFLOPS if args.precision == "fp32" else PEAK_BF16_TFLOPS) * 1e12
     floor_ms = B * sum(max(f / peak_m, b / (PEAK_HBM_GBS * 1e9)) for f, b in costs) * 1e3
     bytes_img = sum(b for _, b in costs)
     achieved = fl_img * B / (body_ms * 1e-3) / 1e12
-    peak = PEAK_BF16_TFLOPS if args.precision == "bf16" else PEAK_F32_TFLOPS
+    peak = PEAK_F32_TFLOPS if args.precision == "fp32" else PEAK_BF16_TFLOPS
     value = world * B * args.steps / elapsed
     out = {
         "metric": METRIC,

@@ -170,7 +170,7 @@ def global_pool(x, mode, p=3.0, eps=1e-6):
     if layout == E.RR_NHWC and c % 4:
         x = x.contiguous()
         layout = E.RR_NCHW
-    if x.dtype not in (torch.float32, torch.bfloat16):
+    if x.dtype not in (torch.float32, torch.bfloat16, torch.float16):
         x = x.float()
     out = torch.empty((n, c), dtype=torch.float32, device=x.device)
     E.check(E.lib().rr_global_pool(E.ptr(x), n, c, h * w, layout, mode, float(p), float(eps), E.ptr(out),

@@ -35,7 +35,8 @@ from .misc import ResidualBlock
 CONV_PARAMS = ["weight"]
 BN_PARAMS = ["weight", "bias", "running_mean", "running_var"]
 
-_PRECISIONS = {"bf16": torch.bfloat16, "fp32": torch.float32, "float32": torch.float32, "bfloat16": torch.bfloat16}
+_PRECISIONS = {"bf16": torch.bfloat16, "fp32": torch.float32, "float32": torch.float32, "bfloat16": torch.bfloat16,
+               "fp16": torch.float16, "float16": torch.float16}
 
 
 def try_index(scalar_or_list, i):
@@ -52,8 +53,11 @@ class _ConvStep:
 class ResNet(nn.Module):
     """Standard residual network (reference ``resnet.py:15-164``).
 
-    Extra (engine) argument: ``precision`` in {"bf16", "fp32"} — the MFMA
-    operand / activation storage type (accumulation is always float32)."""
+    Extra (engine) argument: ``precision`` in {"bf16", "fp16", "fp32"} — the
+    MFMA operand / activation storage type (accumulation is always float32).
+    bf16 runs the fused kernels (stem, direct 3x3, streaming 1x1, boundary
+    pairs); fp16 runs every conv on the generic
+    LDS-DMA implicit-GEMM engine."""
 
     def __init__(self, structure, bottleneck, norm_act=ABN, config=None, classes=0, dilation=1, dropout=None,
                  caffe_mode=False, precision="bf16"):
@@ -150,7 +154,7 @@ class ResNet(nn.Module):
         return super()._load_from_state_dict(*args, **kwargs)
 
     def stem_cin(self):
-        return 8 if self.engine_dtype == torch.bfloat16 else 4
+        return 4 if self.engine_dtype == torch.float32 else 8
 
     def _step(self, conv, bn, cin_pad=None, leaky_override=None):
         st = _ConvStep()
@@ -158,7 +162,8 @@ class ResNet(nn.Module):
         cin_pad = cin_pad or ci
         # engine layout [c_out][(kh*KW + kw)*c_in + ci], 128-B K-steps, rows in the
         # 32-row MFMA-interleaved order so each lane stores 8 consecutive channels
-        st.perm = co % 32 == 0
+        # (fp16 runs the generic LDS-DMA engine on natural-order rows)
+        st.perm = co % 32 == 0 and self.engine_dtype != torch.float16
         st.w = _ops.pack_conv_weights(conv.weight, cin_pad, self.engine_dtype, perm32=st.perm)
         st.kh, st.kw = kh, kw
         st.stride = conv.stride[0]

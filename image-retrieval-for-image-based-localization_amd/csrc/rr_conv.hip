@@ -333,18 +333,39 @@ static bool use_v2(const ConvArgs& a, int dtype) {
 }
 
 template <typename T, typename TO>
-static void dispatch(const ConvArgs& a, bool k1, int dtype, hipStream_t s) {
-    if constexpr (sizeof(T) == 2 && sizeof(TO) == 2) {
-        if (k1 && launch_stream1x1(a, s)) return;
-        if (!k1 && launch_conv3x3(a, s)) return;
+static int dispatch(const ConvArgs& a, bool k1, int dtype, hipStream_t s) {
+    if constexpr (std::is_same<T, bf16_t>::value && std::is_same<TO, bf16_t>::value) {
+        if (k1 && launch_stream1x1(a, s)) return RR_OK;
+        if (!k1 && launch_conv3x3(a, s)) return RR_OK;
     }
-    if (use_v2(a, dtype)) launch_gemm2<T, TO>(a, k1, s);
-    else launch<T, TO>(a, k1, s);
+    if constexpr (std::is_same<T, f16_t>::value) {  // fp16: the LDS-DMA engine only
+        if ((a.kp * 2) % 128 || 256ll * a.kp * 2 >= (1ll << 31))
+            return fail(RR_EINVAL, "rr_conv2d_fused: fp16 needs 128-byte K-steps (k_packed % 64 == 0)");
+        // the engine addresses x through a 31-bit buffer offset: split the batch
+        // into image groups below 2 GiB of input (y / residual are plain pointers)
+        const long long img_bytes = (long long)a.h * a.w_ * a.cin * 2;
+        if (img_bytes >= (1ll << 31)) return fail(RR_EINVAL, "rr_conv2d_fused: one fp16 input image exceeds 2 GiB");
+        const int per = (int)(((1ll << 31) - 1) / img_bytes);
+        const long long opx = (long long)a.ho * a.wo;
+        for (int n0 = 0; n0 < a.n; n0 += per) {
+            ConvArgs c = a;
+            c.n = a.n - n0 < per ? a.n - n0 : per;
+            c.x = (const char*)a.x + n0 * img_bytes;
+            c.y = (char*)a.y + n0 * opx * a.ldy * (long long)sizeof(TO);
+            if (a.res) c.res = (const char*)a.res + n0 * opx * a.ldy * (long long)sizeof(TO);
+            c.P = (int)(c.n * opx);
+            launch_gemm2<T, TO>(c, k1, s);
+        }
+    } else {
+        if (use_v2(a, dtype)) launch_gemm2<T, TO>(a, k1, s);
+        else launch<T, TO>(a, k1, s);
+    }
+    return RR_OK;
 }
 
 void gemm_scores(const ConvArgs& a, int dtype, hipStream_t s) {
     if (dtype == RR_BF16) dispatch<bf16_t, float>(a, true, dtype, s);
-    else if (dtype == RR_F16) launch_gemm2<f16_t, float>(a, true, s);  // LDS-DMA engine only (d >= 64: 128-B K-steps)
+    else if (dtype == RR_F16) dispatch<f16_t, float>(a, true, dtype, s);  // d >= 64: 128-B K-steps
     else dispatch<float, float>(a, true, dtype, s);
 }
 
@@ -357,8 +378,10 @@ extern "C" int rr_conv2d_fused(const void* x, const void* w, const float* scale,
                                void* stream) {
     if (!d) return fail(RR_EINVAL, "rr_conv2d_fused: null desc");
     if (d->c_in <= 0 || (d->c_in & (d->c_in - 1))) return fail(RR_EINVAL, "rr_conv2d_fused: c_in must be a power of two");
-    const int vec = dtype == RR_BF16 ? 8 : 4;
+    const int vec = dtype == RR_F32 ? 4 : 8;
     if (d->c_in < vec) return fail(RR_EINVAL, "rr_conv2d_fused: c_in below one 16-byte chunk");
+    if (dtype == RR_F16 && (d->flags & RR_CONV_PERM32))
+        return fail(RR_EINVAL, "rr_conv2d_fused: fp16 runs natural-order weights (no RR_CONV_PERM32)");
     if (d->k_packed % (4 * vec) != 0 || d->k_packed < d->kh * d->kw * d->c_in)
         return fail(RR_EINVAL, "rr_conv2d_fused: k_packed must cover kh*kw*c_in and be a multiple of 64 bytes");
     if (d->ldy < d->c_out || (d->ldy % 4) != 0) return fail(RR_EINVAL, "rr_conv2d_fused: ldy");
@@ -381,10 +404,14 @@ extern "C" int rr_conv2d_fused(const void* x, const void* w, const float* scale,
     // 1x1 / pad 0: every K-run of a pixel is contiguous -> no im2col index math.
     const bool k1 = d->kh == 1 && d->kw == 1 && d->pad == 0 && d->k_packed == d->c_in;
     hipStream_t s = as_stream(stream);
-    if (dtype == RR_BF16 && out_dtype == RR_BF16) dispatch<bf16_t, bf16_t>(a, k1, dtype, s);
-    else if (dtype == RR_BF16 && out_dtype == RR_F32) dispatch<bf16_t, float>(a, k1, dtype, s);
-    else if (dtype == RR_F32 && out_dtype == RR_F32) dispatch<float, float>(a, k1, dtype, s);
+    int rc;
+    if (dtype == RR_BF16 && out_dtype == RR_BF16) rc = dispatch<bf16_t, bf16_t>(a, k1, dtype, s);
+    else if (dtype == RR_BF16 && out_dtype == RR_F32) rc = dispatch<bf16_t, float>(a, k1, dtype, s);
+    else if (dtype == RR_F16 && out_dtype == RR_F16) rc = dispatch<f16_t, f16_t>(a, k1, dtype, s);
+    else if (dtype == RR_F16 && out_dtype == RR_F32) rc = dispatch<f16_t, float>(a, k1, dtype, s);
+    else if (dtype == RR_F32 && out_dtype == RR_F32) rc = dispatch<float, float>(a, k1, dtype, s);
     else return fail(RR_EINVAL, "rr_conv2d_fused: unsupported dtype pair");
+    if (rc) return rc;
     return check_launch("rr_conv2d_fused");
 }
 
@@ -398,6 +425,9 @@ extern "C" int rr_pack_conv_weights(const float* w, int c_out, int c_in, int kh,
     if (dtype == RR_BF16)
         hipLaunchKernelGGL(k_pack_conv<bf16_t>, dim3(blocks), dim3(256), 0, as_stream(stream), w, c_out, c_in, kh, kw,
                            c_in_pad, k_packed, perm32, (bf16_t*)out);
+    else if (dtype == RR_F16)
+        hipLaunchKernelGGL(k_pack_conv<f16_t>, dim3(blocks), dim3(256), 0, as_stream(stream), w, c_out, c_in, kh, kw,
+                           c_in_pad, k_packed, perm32, (f16_t*)out);
     else if (dtype == RR_F32)
         hipLaunchKernelGGL(k_pack_conv<float>, dim3(blocks), dim3(256), 0, as_stream(stream), w, c_out, c_in, kh, kw,
                            c_in_pad, k_packed, perm32, (float*)out);

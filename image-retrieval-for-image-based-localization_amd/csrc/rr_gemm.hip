@@ -93,6 +93,18 @@ template <> struct St4<bf16_t> {
     }
 };
 
+template <> struct St4<f16_t> {
+    static __device__ __forceinline__ void st(f16_t* p, const float* v) {
+        typedef __attribute__((ext_vector_type(4))) _Float16 h4;
+        *reinterpret_cast<h4*>(p) = (h4){(f16_t)v[0], (f16_t)v[1], (f16_t)v[2], (f16_t)v[3]};
+    }
+    static __device__ __forceinline__ void ld(const f16_t* p, float* v) {
+        typedef __attribute__((ext_vector_type(4))) _Float16 h4;
+        const h4 t = *reinterpret_cast<const h4*>(p);
+        v[0] = (float)t.x; v[1] = (float)t.y; v[2] = (float)t.z; v[3] = (float)t.w;
+    }
+};
+
 // Persistent tile loop: block b walks tiles t = b, b + grid, ... as one
 // flattened stream of (tile, K-step) steps, so the LDS-DMA of the next tile's
 // first K-step is in flight while the current tile's epilogue runs.
@@ -532,7 +544,8 @@ static void launch_ns(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
             hipLaunchKernelGGL((k_igemm<T, TO, TC, TP, WC, WP, 0, PV, NS, AK>), dim3(grid), dim3(64 * WC * WP), 0, s, \
                                a, tiles_p, ntiles, g_xmap ? 1 : 0);                                                  \
     } while (0)
-    if constexpr (sizeof(T) == sizeof(TO) && (TC / WC / 16) % 2 == 0) {
+    // PERM32 epilogue: bf16 only (the fp16 path runs natural-order weights)
+    if constexpr (std::is_same<T, TO>::value && !std::is_same<T, f16_t>::value && (TC / WC / 16) % 2 == 0) {
         if (perm) {
             RR_L3(true);
             return;
@@ -616,6 +629,7 @@ void set_gemm_tuning(int key, int value) {
 template void launch_gemm2<bf16_t, bf16_t>(const ConvArgs&, bool, hipStream_t);
 template void launch_gemm2<bf16_t, float>(const ConvArgs&, bool, hipStream_t);
 template void launch_gemm2<f16_t, float>(const ConvArgs&, bool, hipStream_t);
+template void launch_gemm2<f16_t, f16_t>(const ConvArgs&, bool, hipStream_t);
 template void launch_gemm2<float, float>(const ConvArgs&, bool, hipStream_t);
 
 }  // namespace rr

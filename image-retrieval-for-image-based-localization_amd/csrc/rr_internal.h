@@ -66,6 +66,10 @@ template <> struct DT<bf16_t> {
     static __device__ __forceinline__ float to_f(bf16_t v) { return bf2f(v); }
     static __device__ __forceinline__ bf16_t from_f(float v) { return f2bf(v); }
 };
+template <> struct DT<f16_t> {  // IEEE binary16, round to nearest even
+    static __device__ __forceinline__ float to_f(f16_t v) { return (float)v; }
+    static __device__ __forceinline__ f16_t from_f(float v) { return (f16_t)v; }
+};
 
 // Arguments of the MFMA implicit-GEMM engine (rr_conv.hip); also drives the
 // kNN score GEMM (rr_knn.hip).

@@ -38,6 +38,10 @@ __global__ void __launch_bounds__(256) k_pool_nhwc(const T* __restrict__ x, int 
             if constexpr (sizeof(T) == 4) {
                 float4 t = *reinterpret_cast<const float4*>(q);
                 v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+            } else if constexpr (std::is_same<T, f16_t>::value) {
+                typedef __attribute__((ext_vector_type(4))) _Float16 h4;
+                const h4 t = *reinterpret_cast<const h4*>(q);
+                v[0] = (float)t.x; v[1] = (float)t.y; v[2] = (float)t.z; v[3] = (float)t.w;
             } else {
                 ushort4 t = *reinterpret_cast<const ushort4*>(q);
                 v[0] = bf2f(t.x); v[1] = bf2f(t.y); v[2] = bf2f(t.z); v[3] = bf2f(t.w);
@@ -248,6 +252,8 @@ int rr_global_pool(const void* x, int n, int c, int hw, int layout, int mode, fl
                                mode, p, ip, eps, out);
         else if (dtype == RR_BF16)
             hipLaunchKernelGGL(k_pool_nhwc<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, c, hw, mode, p, ip, eps, out);
+        else if (dtype == RR_F16)
+            hipLaunchKernelGGL(k_pool_nhwc<f16_t>, grid, dim3(256), 0, s, (const f16_t*)x, c, hw, mode, p, ip, eps, out);
         else if (dtype == RR_F32)
             hipLaunchKernelGGL(k_pool_nhwc<float>, grid, dim3(256), 0, s, (const float*)x, c, hw, mode, p, ip, eps, out);
         else
@@ -257,6 +263,8 @@ int rr_global_pool(const void* x, int n, int c, int hw, int layout, int mode, fl
         dim3 grid((unsigned)((planes + 3) / 4));
         if (dtype == RR_BF16)
             hipLaunchKernelGGL(k_pool_nchw<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, planes, hw, mode, p, ip, eps, out);
+        else if (dtype == RR_F16)
+            hipLaunchKernelGGL(k_pool_nchw<f16_t>, grid, dim3(256), 0, s, (const f16_t*)x, planes, hw, mode, p, ip, eps, out);
         else if (dtype == RR_F32)
             hipLaunchKernelGGL(k_pool_nchw<float>, grid, dim3(256), 0, s, (const float*)x, planes, hw, mode, p, ip, eps, out);
         else

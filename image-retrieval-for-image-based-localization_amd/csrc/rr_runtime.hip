@@ -275,6 +275,9 @@ int rr_image_to_nhwc(const float* src, int n, int c, int h, int w, const float* 
     else if (dtype == RR_BF16)
         hipLaunchKernelGGL(k_image_to_nhwc<bf16_t>, dim3(nblk(total, 256)), dim3(256), 0, as_stream(stream), src, n,
                            c, h * w, np, do_normalize, (bf16_t*)dst, c_pad);
+    else if (dtype == RR_F16)
+        hipLaunchKernelGGL(k_image_to_nhwc<f16_t>, dim3(nblk(total, 256)), dim3(256), 0, as_stream(stream), src, n,
+                           c, h * w, np, do_normalize, (f16_t*)dst, c_pad);
     else if (dtype == RR_F32)
         hipLaunchKernelGGL(k_image_to_nhwc<float>, dim3(nblk(total, 256)), dim3(256), 0, as_stream(stream), src, n, c,
                            h * w, np, do_normalize, (float*)dst, c_pad);
@@ -293,6 +296,9 @@ int rr_maxpool2d(const void* x, int n, int h, int w, int c, int k, int stride, i
     else if (dtype == RR_BF16)
         hipLaunchKernelGGL(k_maxpool_nhwc<bf16_t>, dim3(nblk(total, 256)), dim3(256), 0, as_stream(stream),
                            (const bf16_t*)x, n, h, w, c, k, stride, pad, (bf16_t*)y, ho, wo);
+    else if (dtype == RR_F16)
+        hipLaunchKernelGGL(k_maxpool_nhwc<f16_t>, dim3(nblk(total, 256)), dim3(256), 0, as_stream(stream),
+                           (const f16_t*)x, n, h, w, c, k, stride, pad, (f16_t*)y, ho, wo);
     else if (dtype == RR_F32)
         hipLaunchKernelGGL(k_maxpool_nhwc<float>, dim3(nblk(total, 256)), dim3(256), 0, as_stream(stream),
                            (const float*)x, n, h, w, c, k, stride, pad, (float*)y, ho, wo);

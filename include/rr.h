@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-enum rr_dtype { RR_F32 = 0, RR_BF16 = 1, RR_F16 = 2 };  /* RR_F16: kNN screening only */
+enum rr_dtype { RR_F32 = 0, RR_BF16 = 1, RR_F16 = 2 };  /* RR_F16: kNN screening + the generic conv engine (natural-order weights) */
 enum rr_act { RR_ACT_IDENTITY = 0, RR_ACT_LEAKY = 1 };
 enum rr_pool_mode { RR_POOL_GEM = 0, RR_POOL_MAC = 1, RR_POOL_SPOC = 2 };
 enum rr_conv_flags { RR_CONV_AFFINE = 1, RR_CONV_RESIDUAL = 2, RR_CONV_PERM32 = 4 };

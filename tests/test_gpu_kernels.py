@@ -121,9 +121,11 @@ def _check_conv(cuda, case, prec, perm):
     wt = torch.randn(cout, cin, k, k, generator=g) * (2.0 / (cin * k * k)) ** 0.5
     scale = torch.rand(cout, generator=g) + 0.5
     shift = torch.randn(cout, generator=g) * 0.1
-    dtype = torch.float32 if prec == "fp32" else torch.bfloat16
+    dtype = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}[prec]
     if prec == "bf16":
         x, wt = _bf16_round(x), _bf16_round(wt)
+    if prec == "fp16":
+        x, wt = x.half().float(), wt.half().float()
     ref = F.conv2d(x.double(), wt.double(), stride=s, padding=p) * scale.double()[None, :, None, None] \
         + shift.double()[None, :, None, None]
     res = None
@@ -131,11 +133,13 @@ def _check_conv(cuda, case, prec, perm):
         res = torch.randn(ref.shape, generator=g)
         if prec == "bf16":
             res = _bf16_round(res)
+        if prec == "fp16":
+            res = res.half().float()
         ref = ref + res.double()
     if leaky:
         ref = F.leaky_relu(ref, 0.01)
     # engine layout
-    cpad = cin if cin >= 8 else (8 if prec == "bf16" else 4)
+    cpad = cin if cin >= 8 else (4 if prec == "fp32" else 8)
     perm = perm and cout % 32 == 0
     xe = F.pad(x.permute(0, 2, 3, 1), (0, cpad - cin)).contiguous().to(dtype).to(cuda)
     wp = _ops().pack_conv_weights(wt.to(cuda), cpad, dtype, perm32=perm)
@@ -155,11 +159,12 @@ def _check_conv(cuda, case, prec, perm):
     err = (got - ref).abs().max().item()
     scale_ref = ref.abs().max().item()
     # fp32: exact-f32 MFMA chain (K <= 2304): ~1e-6 relative; bf16 output rounding: 2^-8 relative
-    tol = 2e-5 * scale_ref if prec == "fp32" else 8e-3 * scale_ref
+    # fp16 output rounding: 2^-11 relative
+    tol = 2e-5 * scale_ref if prec == "fp32" else (8e-3 if prec == "bf16" else 2e-3) * scale_ref
     assert err <= tol, (err, scale_ref)
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 def test_maxpool(cuda, dtype):
     x = torch.randn(2, 21, 19, 64).to(dtype)
     y = _ops().maxpool2d(x.to(cuda), 3, 2, 1).cpu()
@@ -167,7 +172,7 @@ def test_maxpool(cuda, dtype):
     assert torch.equal(y, ref)
 
 
-@pytest.mark.parametrize("dtype,cpad", [(torch.float32, 4), (torch.bfloat16, 8)])
+@pytest.mark.parametrize("dtype,cpad", [(torch.float32, 4), (torch.bfloat16, 8), (torch.float16, 8)])
 def test_image_to_nhwc(cuda, dtype, cpad):
     """normalise (cirtorch/utils/image.py:125) + NCHW->NHWC + zero channel pad."""
     x = torch.rand(2, 3, 13, 17)
@@ -339,3 +344,48 @@ def test_conv1x1_pair_projection(cuda, c_out):
     gz = z.float().permute(0, 3, 1, 2).cpu().double()
     assert (gy - yr).abs().max().item() <= 8e-3 * yr.abs().max().item()
     assert (gz - zr).abs().max().item() <= 1.6e-2 * zr.abs().max().item()
+
+
+FP16_CASES = [
+    # the generic LDS-DMA engine in fp16 (natural-order weights): 1x1, strided 1x1,
+    # 3x3 s1/s2, the 7x7/s2 stem shape on 8 padded channels, residual + leaky
+    (2, 64, 17, 23, 256, 1, 1, 0, True, True),
+    (2, 256, 18, 22, 512, 1, 2, 0, False, False),
+    (2, 64, 16, 32, 64, 3, 1, 1, False, True),
+    (1, 128, 19, 21, 128, 3, 2, 1, False, True),
+    (1, 3, 45, 61, 64, 7, 2, 3, False, True),
+    (1, 512, 9, 11, 2048, 1, 1, 0, True, True),
+]
+
+
+@pytest.mark.parametrize("case", FP16_CASES)
+def test_conv_fp16_generic_engine(cuda, case):
+    _check_conv(cuda, case, "fp16", False)
+
+
+def test_conv_fp16_splits_large_batches(cuda):
+    """> 2 GiB of fp16 input: the launch is split into image groups (31-bit
+    buffer offsets); each group must equal the same images run alone."""
+    g = torch.Generator(device="cpu").manual_seed(3)
+    n, h, w, c = 9, 256, 256, 2048                        # 9 x 256 MiB = 2.25 GiB
+    x = torch.empty(n, h, w, c, dtype=torch.float16, device=cuda)
+    for i in range(n):
+        x[i] = (torch.randn(h, w, c, generator=g) * 0.5).half().to(cuda)
+    wt = torch.randn(64, c, 1, 1, generator=g) * c ** -0.5
+    wp = _ops().pack_conv_weights(wt.to(cuda), c, torch.float16)
+    y = _ops().conv2d_fused(x, wp, 1, 1, 1, 0, 64, leaky=False)
+    for i in (0, 7, 8):
+        yi = _ops().conv2d_fused(x[i:i + 1].contiguous(), wp, 1, 1, 1, 0, 64, leaky=False)
+        assert torch.equal(y[i:i + 1], yi)
+    del x
+
+
+def test_conv_fp16_rejects_perm32(cuda):
+    import ctypes
+    from cirtorch import _engine as E
+    x = torch.zeros(1, 4, 4, 64, dtype=torch.float16, device=cuda)
+    w = torch.zeros(64, 64, dtype=torch.float16, device=cuda)
+    y = torch.empty(16, 64, dtype=torch.float16, device=cuda)
+    d = E.ConvDesc(1, 4, 4, 64, 4, 4, 64, 1, 1, 1, 0, 1, 64, 64, 0, 0.0, E.RR_CONV_PERM32)
+    rc = E.lib().rr_conv2d_fused(E.ptr(x), E.ptr(w), None, None, None, E.ptr(y), ctypes.byref(d), 2, 2, None)
+    assert rc == -1 and b"PERM32" in E.lib().rr_last_error()

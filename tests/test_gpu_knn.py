@@ -96,7 +96,7 @@ def test_topk_merge_equals_single_shard(cuda):
 
 def test_fp16_screening_copy_and_limits(cuda):
     """The fp16 screening copy is IEEE binary16 round-to-nearest-even (== torch
-    .half()); fp16 screening needs d >= 64 and is rejected by the conv engine."""
+    .half()); fp16 screening needs d >= 64; the bf16-only fused kernels reject it."""
     from cirtorch import _ops
     from cirtorch import _engine as E
     from cirtorch.search import KnnIndex
@@ -107,11 +107,10 @@ def test_fp16_screening_copy_and_limits(cuda):
     with pytest.raises(RuntimeError, match="d >= 64"):
         KnnIndex(db, "fp16").search(db[:2], 3)
     xh = torch.zeros(1, 4, 4, 64, dtype=torch.float16, device=cuda)
-    w = torch.zeros(64, 64, dtype=torch.float16, device=cuda)
-    y = torch.empty(16, 64, dtype=torch.float16, device=cuda)
-    d = E.ConvDesc(1, 4, 4, 64, 4, 4, 64, 1, 1, 1, 0, 1, 64, 64, 0, 0.0, 0)
-    rc = E.lib().rr_conv2d_fused(E.ptr(xh), E.ptr(w), None, None, None, E.ptr(y), ctypes.byref(d), 2, 2, None)
-    assert rc == -1 and b"dtype" in E.lib().rr_last_error()
+    y = torch.empty(1, 4, 4, 64, dtype=torch.float16, device=cuda)
+    rc = E.lib().rr_conv1x1_pair(E.ptr(xh), 16, 64, None, None, None, 256, None, None, None, None, None, 0, 0.0,
+                                 None, None, None, 64, 0, 0.0, E.ptr(y), E.ptr(y), 2, None)
+    assert rc == -1 and b"bf16 only" in E.lib().rr_last_error()
 
 
 def test_knn_full_size_1m_bench_shape(cuda):
