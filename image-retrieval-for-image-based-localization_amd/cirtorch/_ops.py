@@ -111,19 +111,21 @@ def maxpool2d(x, k=3, stride=2, pad=1):
     return y
 
 
-def pack_stem_weights(weight):
-    """conv1 weight [64, 3, 7, 7] (GPU) -> the fused stem's bf16 [64, 256] layout."""
+def pack_stem_weights(weight, dtype=torch.bfloat16):
+    """conv1 weight [64, 3, 7, 7] (GPU) -> the fused stem's [64, 256] layout (bf16 or fp16)."""
     E.require_gpu(weight)
     w = weight.detach().float().contiguous()
     co, ci, kh, kw = w.shape
-    out = torch.empty((co, 256), dtype=torch.bfloat16, device=w.device)
-    E.check(E.lib().rr_stem_pack_weights(E.ptr(w), co, ci, kh, kw, E.ptr(out), _st()), "rr_stem_pack_weights")
+    out = torch.empty((co, 256), dtype=dtype, device=w.device)
+    E.check(E.lib().rr_stem_pack_weights(E.ptr(w), co, ci, kh, kw, E.ptr(out), E.dtype_code(dtype), _st()),
+            "rr_stem_pack_weights")
     return out
 
 
 def stem_conv_pool(img, wpk, scale, shift, leaky=True, slope=0.01, mean=None, std=None):
     """Fused normalise + conv1 7x7/s2/p3 + BN + act + maxpool 3x3/s2/p1
-    (cirtorch/backbones/resnet.py:59-66): [N, 3, H, W] float32 -> [N, Hp, Wp, 64] bf16."""
+    (cirtorch/backbones/resnet.py:59-66): [N, 3, H, W] float32 -> [N, Hp, Wp, 64] in wpk's dtype
+    (bf16 or fp16)."""
     E.require_gpu(img, wpk, scale, shift)
     img = img.contiguous().float()
     n, c, h, w = img.shape
@@ -131,13 +133,13 @@ def stem_conv_pool(img, wpk, scale, shift, leaky=True, slope=0.01, mean=None, st
         raise RuntimeError("stem_conv_pool: expected 3-channel images, got %d" % c)
     ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
     hp, wp = (ho - 1) // 2 + 1, (wo - 1) // 2 + 1
-    y = torch.empty((n, hp, wp, 64), dtype=torch.bfloat16, device=img.device)
+    y = torch.empty((n, hp, wp, 64), dtype=wpk.dtype, device=img.device)
     do = mean is not None
     m = (ctypes.c_float * 3)(*mean) if do else (ctypes.c_float * 3)()
     s = (ctypes.c_float * 3)(*std) if do else (ctypes.c_float * 3)(1, 1, 1)
     E.check(E.lib().rr_stem_conv_pool(E.ptr(img), n, h, w, m, s, int(do), E.ptr(wpk), E.ptr(scale), E.ptr(shift),
                                       E.RR_ACT_LEAKY if leaky else E.RR_ACT_IDENTITY, float(slope), E.ptr(y), hp, wp,
-                                      _st()), "rr_stem_conv_pool")
+                                      E.dtype_code(wpk.dtype), _st()), "rr_stem_conv_pool")
     return y
 
 

@@ -55,9 +55,9 @@ class ResNet(nn.Module):
 
     Extra (engine) argument: ``precision`` in {"bf16", "fp16", "fp32"} — the
     MFMA operand / activation storage type (accumulation is always float32).
-    bf16 runs the fused kernels (stem, direct 3x3, streaming 1x1, boundary
-    pairs); fp16 runs every conv on the generic
-    LDS-DMA implicit-GEMM engine."""
+    bf16 and fp16 run the fused kernels (stem, direct
+    3x3, streaming 1x1, boundary pairs); fp32 is the exact-f32 MFMA parity
+    mode."""
 
     def __init__(self, structure, bottleneck, norm_act=ABN, config=None, classes=0, dilation=1, dropout=None,
                  caffe_mode=False, precision="bf16"):
@@ -162,8 +162,7 @@ class ResNet(nn.Module):
         cin_pad = cin_pad or ci
         # engine layout [c_out][(kh*KW + kw)*c_in + ci], 128-B K-steps, rows in the
         # 32-row MFMA-interleaved order so each lane stores 8 consecutive channels
-        # (fp16 runs the generic LDS-DMA engine on natural-order rows)
-        st.perm = co % 32 == 0 and self.engine_dtype != torch.float16
+        st.perm = co % 32 == 0
         st.w = _ops.pack_conv_weights(conv.weight, cin_pad, self.engine_dtype, perm32=st.perm)
         st.kh, st.kw = kh, kw
         st.stride = conv.stride[0]
@@ -180,11 +179,11 @@ class ResNet(nn.Module):
         if dev.type != "cuda":
             raise RuntimeError("the MI355X engine runs on the GPU: call .cuda() on the model first")
         plan = {"stem": self._step(self.mod1.conv1, self.mod1.bn1, cin_pad=self.stem_cin()), "mods": []}
-        # bf16: conv1 + bn1 + pool1 run as ONE fused kernel (rr_stem_conv_pool)
+        # bf16 / fp16: conv1 + bn1 + pool1 run as ONE fused kernel (rr_stem_conv_pool)
         plan["stem_fused"] = None
-        if self.engine_dtype == torch.bfloat16 and tuple(self.mod1.conv1.weight.shape) == (64, 3, 7, 7) \
+        if self.engine_dtype in (torch.bfloat16, torch.float16) and tuple(self.mod1.conv1.weight.shape) == (64, 3, 7, 7) \
                 and hasattr(self.mod1, "pool1") and os.environ.get("RR_STEM_FUSED", "1") != "0":
-            plan["stem_fused"] = _ops.pack_stem_weights(self.mod1.conv1.weight)
+            plan["stem_fused"] = _ops.pack_stem_weights(self.mod1.conv1.weight, self.engine_dtype)
         for mod_id in range(4):
             mod = getattr(self, "mod%d" % (mod_id + 2))
             blocks = []
@@ -253,8 +252,8 @@ class ResNet(nn.Module):
 
     def _pairable(self, last, nxt):
         """conv3 of a 64->256 bottleneck followed by a stride-1 1x1 conv1 (256 -> 64/128):
-        one fused rr_conv1x1_pair launch (bf16)."""
-        if nxt is None or self.engine_dtype != torch.bfloat16 or os.environ.get("RR_PAIR_FUSED", "1") == "0":
+        one fused rr_conv1x1_pair launch (bf16 / fp16)."""
+        if nxt is None or self.engine_dtype == torch.float32 or os.environ.get("RR_PAIR_FUSED", "1") == "0":
             return False
         return (last.kh == 1 and last.stride == 1 and last.perm and last.c_out == 256 and last.w.shape[1] == 64
                 and nxt.kh == 1 and nxt.stride == 1 and nxt.pad == 0 and nxt.perm and nxt.w.shape[1] == 256

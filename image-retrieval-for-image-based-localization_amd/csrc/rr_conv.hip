@@ -297,8 +297,8 @@ static void launch(const ConvArgs& a, bool k1, hipStream_t s) {
 }
 
 template <typename T, typename TO> void launch_gemm2(const ConvArgs& a, bool k1, hipStream_t s);
-bool launch_stream1x1(const ConvArgs& a, hipStream_t s);  // rr_stream.hip
-bool launch_conv3x3(const ConvArgs& a, hipStream_t s);    // rr_conv3.hip
+bool launch_stream1x1(const ConvArgs& a, hipStream_t s, bool f16);  // rr_stream.hip
+bool launch_conv3x3(const ConvArgs& a, hipStream_t s, bool f16);    // rr_conv3.hip
 extern int g_stream_mode;
 extern int g_conv3_mode;
 
@@ -334,9 +334,10 @@ static bool use_v2(const ConvArgs& a, int dtype) {
 
 template <typename T, typename TO>
 static int dispatch(const ConvArgs& a, bool k1, int dtype, hipStream_t s) {
-    if constexpr (std::is_same<T, bf16_t>::value && std::is_same<TO, bf16_t>::value) {
-        if (k1 && launch_stream1x1(a, s)) return RR_OK;
-        if (!k1 && launch_conv3x3(a, s)) return RR_OK;
+    if constexpr (sizeof(T) == 2 && std::is_same<T, TO>::value) {  // bf16 / fp16 fused kernels
+        constexpr bool f16 = std::is_same<T, f16_t>::value;
+        if (k1 && launch_stream1x1(a, s, f16)) return RR_OK;
+        if (!k1 && launch_conv3x3(a, s, f16)) return RR_OK;
     }
     if constexpr (std::is_same<T, f16_t>::value) {  // fp16: the LDS-DMA engine only
         if ((a.kp * 2) % 128 || 256ll * a.kp * 2 >= (1ll << 31))
@@ -380,8 +381,6 @@ extern "C" int rr_conv2d_fused(const void* x, const void* w, const float* scale,
     if (d->c_in <= 0 || (d->c_in & (d->c_in - 1))) return fail(RR_EINVAL, "rr_conv2d_fused: c_in must be a power of two");
     const int vec = dtype == RR_F32 ? 4 : 8;
     if (d->c_in < vec) return fail(RR_EINVAL, "rr_conv2d_fused: c_in below one 16-byte chunk");
-    if (dtype == RR_F16 && (d->flags & RR_CONV_PERM32))
-        return fail(RR_EINVAL, "rr_conv2d_fused: fp16 runs natural-order weights (no RR_CONV_PERM32)");
     if (d->k_packed % (4 * vec) != 0 || d->k_packed < d->kh * d->kw * d->c_in)
         return fail(RR_EINVAL, "rr_conv2d_fused: k_packed must cover kh*kw*c_in and be a multiple of 64 bytes");
     if (d->ldy < d->c_out || (d->ldy % 4) != 0) return fail(RR_EINVAL, "rr_conv2d_fused: ldy");

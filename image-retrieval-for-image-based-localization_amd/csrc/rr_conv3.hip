@@ -32,7 +32,6 @@ namespace rr {
 
 namespace {
 
-typedef __attribute__((ext_vector_type(8))) __bf16 pbf16x8_t;
 typedef __attribute__((ext_vector_type(4))) float pf32x4_t;
 typedef __attribute__((ext_vector_type(4))) int pi32x4_t;
 
@@ -83,7 +82,7 @@ struct TileC {
     int ct, img, oh0, ow0;
 };
 
-template <int TC, int TH, int TW, int WC, int WP, bool ARES, int NSA>
+template <int TC, int TH, int TW, int WC, int WP, bool ARES, int NSA, typename HT>
 __global__ void __launch_bounds__(64 * WC * WP) k_conv3x3(ConvArgs a, int tiles_w, int tiles_hw, int tiles_c,
                                                          int ntiles) {
     constexpr int NW = WC * WP, NT = 64 * NW;
@@ -191,9 +190,7 @@ __global__ void __launch_bounds__(64 * WC * WP) k_conv3x3(ConvArgs a, int tiles_
             for (int i = 0; i < FM; ++i)
 #pragma unroll
                 for (int j = 0; j < FN; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(pbf16x8_t, fa[i]),
-                                                                        __builtin_bit_cast(pbf16x8_t, fb[j]),
-                                                                        acc[i][j], 0, 0, 0);
+                    acc[i][j] = H16<HT>::mfma(fa[i], fb[j], acc[i][j]);
         }
     };
 
@@ -227,10 +224,10 @@ __global__ void __launch_bounds__(64 * WC * WP) k_conv3x3(ConvArgs a, int tiles_
                     for (int r = 0; r < 8; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * slope;
                 }
                 uint4 o;
-                o.x = pack_bf16x2(v[0], v[1]);
-                o.y = pack_bf16x2(v[2], v[3]);
-                o.z = pack_bf16x2(v[4], v[5]);
-                o.w = pack_bf16x2(v[6], v[7]);
+                o.x = H16<HT>::pack2(v[0], v[1]);
+                o.y = H16<HT>::pack2(v[2], v[3]);
+                o.z = H16<HT>::pack2(v[4], v[5]);
+                o.w = H16<HT>::pack2(v[6], v[7]);
                 *reinterpret_cast<uint4*>(Y + pix * a.ldy + c) = o;
             }
         }
@@ -327,13 +324,17 @@ __global__ void __launch_bounds__(64 * WC * WP) k_conv3x3(ConvArgs a, int tiles_
 }
 
 template <int TC, int TH, int TW, int WC, int WP, bool ARES, int NSA = 2>
-void launch_c3(const ConvArgs& a, hipStream_t s) {
+void launch_c3(const ConvArgs& a, hipStream_t s, bool f16) {
     const int tiles_w = a.w_ / TW, tiles_h = a.h / TH, tiles_c = a.cout / TC;
     const long long ntl = (long long)a.n * tiles_h * tiles_w * tiles_c;
     const int cus = grid_cus();
     const int grid = (int)(ntl < cus ? ntl : cus);
-    hipLaunchKernelGGL((k_conv3x3<TC, TH, TW, WC, WP, ARES, NSA>), dim3(grid), dim3(64 * WC * WP), 0, s, a, tiles_w,
-                       tiles_w * tiles_h, tiles_c, (int)ntl);
+    if (f16)
+        hipLaunchKernelGGL((k_conv3x3<TC, TH, TW, WC, WP, ARES, NSA, f16_t>), dim3(grid), dim3(64 * WC * WP), 0, s, a,
+                           tiles_w, tiles_w * tiles_h, tiles_c, (int)ntl);
+    else
+        hipLaunchKernelGGL((k_conv3x3<TC, TH, TW, WC, WP, ARES, NSA, bf16_t>), dim3(grid), dim3(64 * WC * WP), 0, s, a,
+                           tiles_w, tiles_w * tiles_h, tiles_c, (int)ntl);
 }
 
 }  // namespace
@@ -345,7 +346,7 @@ int g_conv3_mode = 1;  // rr_set_tuning(RR_TUNE_CONV3X3): 0 off, 1 auto, 2 / 3 p
 // bf16 3x3 / stride 1 / pad 1 with PERM32 weights, bf16 out, no residual, and
 // image sizes the tiles divide; returns false otherwise (caller falls back to
 // the implicit-GEMM engine).
-bool launch_conv3x3(const ConvArgs& a, hipStream_t s) {
+bool launch_conv3x3(const ConvArgs& a, hipStream_t s, bool f16) {
     if (g_conv3_mode == 0) return false;
     if (a.kh != 3 || a.kw != 3 || a.stride != 1 || a.pad != 1 || a.dil != 1) return false;
     if (!(a.flags & RR_CONV_PERM32) || (a.flags & RR_CONV_RESIDUAL) || a.ldy != a.cout) return false;
@@ -355,9 +356,9 @@ bool launch_conv3x3(const ConvArgs& a, hipStream_t s) {
     const int g_c3_cus = grid_cus();
     if (a.cin == 64 && a.cout == 64 && a.h % 8 == 0) {
         // 8 waves (2 per SIMD) measured fastest: 125 us vs 146 (4 waves) at 32 x 192x256x64
-        if (g_conv3_mode == 4) launch_c3<64, 8, 32, 1, 8, true>(a, s);
-        else if (g_conv3_mode == 6) launch_c3<64, 8, 32, 1, 4, true>(a, s);
-        else launch_c3<64, 8, 32, 2, 4, true>(a, s);
+        if (g_conv3_mode == 4) launch_c3<64, 8, 32, 1, 8, true>(a, s, f16);
+        else if (g_conv3_mode == 6) launch_c3<64, 8, 32, 1, 4, true>(a, s, f16);
+        else launch_c3<64, 8, 32, 2, 4, true>(a, s, f16);
         return true;
     }
     if (a.cout % 128 == 0 && a.cout <= 512) {
@@ -369,18 +370,18 @@ bool launch_conv3x3(const ConvArgs& a, hipStream_t s) {
         // tiles, 48 MFMAs per wave between barriers) for c_out % 256 == 0
         // (measured at 128 x R50: mod4 c2 505 -> 461 us, mod5 c2 472 -> 416 us; default where it applies)
         if ((g_conv3_mode == 1 || g_conv3_mode == 8) && a.cout % 256 == 0 && a.h % 6 == 0) {
-            launch_c3<256, 6, 32, 4, 2, false>(a, s);
+            launch_c3<256, 6, 32, 4, 2, false>(a, s, f16);
             return true;
         }
         const bool deep = g_conv3_mode == 7;  // 3-stage weight ring
         if (t8 > 0 && (want8 || a.h % 4 != 0)) {
-            if (deep) launch_c3<128, 8, 32, 2, 4, false, 3>(a, s);
-            else launch_c3<128, 8, 32, 2, 4, false>(a, s);
+            if (deep) launch_c3<128, 8, 32, 2, 4, false, 3>(a, s, f16);
+            else launch_c3<128, 8, 32, 2, 4, false>(a, s, f16);
             return true;
         }
         if (a.h % 4 == 0) {
-            if (deep) launch_c3<128, 4, 32, 2, 4, false, 3>(a, s);
-            else launch_c3<128, 4, 32, 2, 4, false>(a, s);
+            if (deep) launch_c3<128, 4, 32, 2, 4, false, 3>(a, s, f16);
+            else launch_c3<128, 4, 32, 2, 4, false>(a, s, f16);
             return true;
         }
     }

@@ -338,8 +338,8 @@ __global__ void __launch_bounds__(64 * WC * WP, ((NS == 2 && AK * TC <= 256) || 
                             const unsigned w4[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
                             for (int r = 0; r < 4; ++r) {
-                                rv[2 * r] = __uint_as_float(w4[r] << 16);
-                                rv[2 * r + 1] = __uint_as_float(w4[r] & 0xffff0000u);
+                                rv[2 * r] = H16<TO>::lo(w4[r]);
+                                rv[2 * r + 1] = H16<TO>::hi(w4[r]);
                             }
                         } else {
                             St4<TO>::ld(R + o, rv);
@@ -354,10 +354,10 @@ __global__ void __launch_bounds__(64 * WC * WP, ((NS == 2 && AK * TC <= 256) || 
                     }
                     if constexpr (sizeof(TO) == 2) {
                         uint4 q;
-                        q.x = pack_bf16x2(v[0], v[1]);
-                        q.y = pack_bf16x2(v[2], v[3]);
-                        q.z = pack_bf16x2(v[4], v[5]);
-                        q.w = pack_bf16x2(v[6], v[7]);
+                        q.x = H16<TO>::pack2(v[0], v[1]);
+                        q.y = H16<TO>::pack2(v[2], v[3]);
+                        q.z = H16<TO>::pack2(v[4], v[5]);
+                        q.w = H16<TO>::pack2(v[6], v[7]);
                         *reinterpret_cast<uint4*>(Y + o) = q;
                     } else {
                         St4<TO>::st(Y + o, v);
@@ -544,8 +544,7 @@ static void launch_ns(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
             hipLaunchKernelGGL((k_igemm<T, TO, TC, TP, WC, WP, 0, PV, NS, AK>), dim3(grid), dim3(64 * WC * WP), 0, s, \
                                a, tiles_p, ntiles, g_xmap ? 1 : 0);                                                  \
     } while (0)
-    // PERM32 epilogue: bf16 only (the fp16 path runs natural-order weights)
-    if constexpr (std::is_same<T, TO>::value && !std::is_same<T, f16_t>::value && (TC / WC / 16) % 2 == 0) {
+    if constexpr (std::is_same<T, TO>::value && (TC / WC / 16) % 2 == 0) {
         if (perm) {
             RR_L3(true);
             return;

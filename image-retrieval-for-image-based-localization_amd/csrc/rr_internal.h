@@ -66,6 +66,35 @@ template <> struct DT<bf16_t> {
     static __device__ __forceinline__ float to_f(bf16_t v) { return bf2f(v); }
     static __device__ __forceinline__ bf16_t from_f(float v) { return f2bf(v); }
 };
+// 16-bit MFMA operand types of the fused kernels (bf16 or IEEE fp16): one
+// v_mfma_f32_16x16x32_{bf16,f16} on 8 packed values per lane, packing of two
+// floats (round to nearest even) and unpacking of a packed pair.
+typedef __attribute__((ext_vector_type(4))) float h16_f32x4_t;
+template <typename H> struct H16;
+template <> struct H16<bf16_t> {
+    typedef __attribute__((ext_vector_type(8))) __bf16 v8;
+    static __device__ __forceinline__ h16_f32x4_t mfma(uint4 a, uint4 b, h16_f32x4_t c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8, a), __builtin_bit_cast(v8, b), c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ uint32_t pack2(float lo, float hi) { return pack_bf16x2(lo, hi); }
+    static __device__ __forceinline__ float lo(uint32_t w) { return __uint_as_float(w << 16); }
+    static __device__ __forceinline__ float hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+    static constexpr uint32_t NEG_INF = 0xFF80u;
+};
+template <> struct H16<f16_t> {
+    typedef __attribute__((ext_vector_type(8))) _Float16 v8;
+    typedef __attribute__((ext_vector_type(2))) _Float16 v2;
+    static __device__ __forceinline__ h16_f32x4_t mfma(uint4 a, uint4 b, h16_f32x4_t c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(v8, a), __builtin_bit_cast(v8, b), c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ uint32_t pack2(float lo, float hi) {
+        return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_cvt_t){lo, hi}, v2));
+    }
+    static __device__ __forceinline__ float lo(uint32_t w) { return (float)__builtin_bit_cast(v2, w).x; }
+    static __device__ __forceinline__ float hi(uint32_t w) { return (float)__builtin_bit_cast(v2, w).y; }
+    static constexpr uint32_t NEG_INF = 0xFC00u;
+};
+
 template <> struct DT<f16_t> {  // IEEE binary16, round to nearest even
     static __device__ __forceinline__ float to_f(f16_t v) { return (float)v; }
     static __device__ __forceinline__ f16_t from_f(float v) { return (f16_t)v; }

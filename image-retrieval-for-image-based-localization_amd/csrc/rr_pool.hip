@@ -77,7 +77,8 @@ __global__ void __launch_bounds__(256) k_pool_nhwc(const T* __restrict__ x, int 
 // channels per lane, a wave covers 512 channels of one pixel, the block's 16
 // waves split the pixels (4 loads in flight per lane); the 16 partials are
 // combined through LDS in a fixed order.  grid = (ceil(c/512), n).
-__global__ void __launch_bounds__(1024) k_pool_nhwc_bf16x8(const uint4* __restrict__ x, int c, int hw, int mode,
+template <typename H>
+__global__ void __launch_bounds__(1024) k_pool_nhwc_h16x8(const uint4* __restrict__ x, int c, int hw, int mode,
                                                            float p, int ip, float eps, float* __restrict__ out) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int c8 = c >> 3;
@@ -92,7 +93,7 @@ __global__ void __launch_bounds__(1024) k_pool_nhwc_bf16x8(const uint4* __restri
         const unsigned u[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            const float v0 = __uint_as_float(u[e] << 16), v1 = __uint_as_float(u[e] & 0xffff0000u);
+            const float v0 = H16<H>::lo(u[e]), v1 = H16<H>::hi(u[e]);
             if (mode == RR_POOL_GEM) {
                 acc[2 * e] += powp(fmaxf(v0, eps), p, ip);
                 acc[2 * e + 1] += powp(fmaxf(v1, eps), p, ip);
@@ -248,8 +249,11 @@ int rr_global_pool(const void* x, int n, int c, int hw, int layout, int mode, fl
         if (c % 4) return fail(RR_EINVAL, "rr_global_pool: NHWC needs c % 4 == 0");
         dim3 grid((c + 255) / 256, n);
         if (dtype == RR_BF16 && c % 8 == 0 && ((uintptr_t)x & 15) == 0)
-            hipLaunchKernelGGL(k_pool_nhwc_bf16x8, dim3((c + 511) / 512, n), dim3(1024), 0, s, (const uint4*)x, c, hw,
+            hipLaunchKernelGGL(k_pool_nhwc_h16x8<bf16_t>, dim3((c + 511) / 512, n), dim3(1024), 0, s, (const uint4*)x, c, hw,
                                mode, p, ip, eps, out);
+        else if (dtype == RR_F16 && c % 8 == 0 && ((uintptr_t)x & 15) == 0)
+            hipLaunchKernelGGL(k_pool_nhwc_h16x8<f16_t>, dim3((c + 511) / 512, n), dim3(1024), 0, s, (const uint4*)x, c,
+                               hw, mode, p, ip, eps, out);
         else if (dtype == RR_BF16)
             hipLaunchKernelGGL(k_pool_nhwc<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, c, hw, mode, p, ip, eps, out);
         else if (dtype == RR_F16)

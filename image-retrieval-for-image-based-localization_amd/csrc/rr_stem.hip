@@ -27,7 +27,6 @@ namespace rr {
 
 namespace {
 
-typedef __attribute__((ext_vector_type(8))) __bf16 tbf16x8_t;
 typedef __attribute__((ext_vector_type(4))) float tf32x4_t;
 
 struct StemArgs {
@@ -54,9 +53,11 @@ __device__ __forceinline__ unsigned bf16_key2(unsigned w) {
     return w ^ (neg * 0x7FFFu);
 }
 
-template <int PH, int PW>
+template <int PH, int PW, typename HT>
 __global__ void __launch_bounds__(NT) k_stem_pool(StemArgs a, int tiles_w, int tiles_hw, int ntiles) {
     constexpr int SR = 2 * PH + 1, SC = 2 * PW + 1, NP = SR * SC, NF = (NP + 15) / 16;
+    constexpr unsigned KNI = H16<HT>::NEG_INF ^ 0x7FFFu;  // order key of -inf (pool padding)
+    constexpr unsigned KNI2 = KNI | (KNI << 16);
     constexpr int IR = 2 * (SR - 1) + 7, IC = 2 * (SC - 1) + 8;  // IC even: 16-B aligned pixel pairs
     constexpr int NSLOT = IR * IC, SPT = (NSLOT + NT - 1) / NT;
     constexpr int PATCH = NSLOT * 8;
@@ -122,8 +123,8 @@ __global__ void __launch_bounds__(NT) k_stem_pool(StemArgs a, int tiles_w, int t
             for (int ch = 0; ch < 3; ++ch)  // zero padding is applied AFTER normalisation
                 v[ch] = (ok && a.do_norm) ? (pf[u][ch] - a.mean[ch]) * a.rstd[ch] : pf[u][ch];
             uint2 o;
-            o.x = pack_bf16x2(v[0], v[1]);
-            o.y = pack_bf16x2(v[2], 0.f);
+            o.x = H16<HT>::pack2(v[0], v[1]);
+            o.y = H16<HT>::pack2(v[2], 0.f);
             *reinterpret_cast<uint2*>(sP[buf] + slot * 8) = o;
         }
     };
@@ -154,8 +155,7 @@ __global__ void __launch_bounds__(NT) k_stem_pool(StemArgs a, int tiles_w, int t
                 const uint4 b = *reinterpret_cast<const uint4*>(pb + m * IC * 8);
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
-                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(tbf16x8_t, areg[i][m]),
-                                                                    __builtin_bit_cast(tbf16x8_t, b), acc[i], 0, 0, 0);
+                    acc[i] = H16<HT>::mfma(areg[i][m], b, acc[i]);
             }
             const bool valid = (unsigned)(sr0 + sr) < (unsigned)a.ho && (unsigned)(sc0 + sc) < (unsigned)a.wo;
             if (n < NP) {
@@ -174,12 +174,12 @@ __global__ void __launch_bounds__(NT) k_stem_pool(StemArgs a, int tiles_w, int t
                     }
                     uint4 o;
                     if (valid) {
-                        o.x = bf16_key2(pack_bf16x2(v[0], v[1]));
-                        o.y = bf16_key2(pack_bf16x2(v[2], v[3]));
-                        o.z = bf16_key2(pack_bf16x2(v[4], v[5]));
-                        o.w = bf16_key2(pack_bf16x2(v[6], v[7]));
+                        o.x = bf16_key2(H16<HT>::pack2(v[0], v[1]));
+                        o.y = bf16_key2(H16<HT>::pack2(v[2], v[3]));
+                        o.z = bf16_key2(H16<HT>::pack2(v[4], v[5]));
+                        o.w = bf16_key2(H16<HT>::pack2(v[6], v[7]));
                     } else {
-                        o = make_uint4(0x807F807Fu, 0x807F807Fu, 0x807F807Fu, 0x807F807Fu);  // key(-inf): pool padding
+                        o = make_uint4(KNI2, KNI2, KNI2, KNI2);  // key(-inf): pool padding
                     }
                     const int chunk = 4 * i2 + q;
                     *reinterpret_cast<uint4*>(sO + n * 128 + ((chunk ^ (n & 7)) << 4)) = o;
@@ -200,7 +200,7 @@ __global__ void __launch_bounds__(NT) k_stem_pool(StemArgs a, int tiles_w, int t
             // two channels per v_pk_max_i16
             short2v mx[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) mx[j] = (short2v){(short)0x807F, (short)0x807F};
+            for (int j = 0; j < 4; ++j) mx[j] = (short2v){(short)KNI, (short)KNI};
 #pragma unroll
             for (int dr = 0; dr < 3; ++dr)
 #pragma unroll
@@ -224,7 +224,8 @@ __global__ void __launch_bounds__(NT) k_stem_pool(StemArgs a, int tiles_w, int t
 }
 
 // out[R][k], R packed row (PERM32), k = kh*32 + kw*4 + ci (kh < 7, kw < 7, ci < 3 real; rest 0)
-__global__ void k_stem_pack(const float* __restrict__ w, bf16_t* __restrict__ out) {
+template <typename HT>
+__global__ void k_stem_pack(const float* __restrict__ w, HT* __restrict__ out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= 64 * 256) return;
     const int R = i >> 8, k = i & 255;
@@ -232,7 +233,7 @@ __global__ void k_stem_pack(const float* __restrict__ w, bf16_t* __restrict__ ou
     const int kh = k >> 5, kw = (k >> 2) & 7, ci = k & 3;
     float v = 0.f;
     if (kh < 7 && kw < 7 && ci < 3) v = w[((co * 3 + ci) * 7 + kh) * 7 + kw];
-    out[i] = f2bf(v);
+    out[i] = DT<HT>::from_f(v);
 }
 
 
@@ -242,17 +243,23 @@ __global__ void k_stem_pack(const float* __restrict__ w, bf16_t* __restrict__ ou
 
 using namespace rr;
 
-extern "C" int rr_stem_pack_weights(const float* w, int c_out, int c_in, int kh, int kw, void* out, void* stream) {
+extern "C" int rr_stem_pack_weights(const float* w, int c_out, int c_in, int kh, int kw, void* out, int dtype,
+                                    void* stream) {
+    if (dtype != RR_BF16 && dtype != RR_F16) return fail(RR_EINVAL, "rr_stem_pack_weights: bf16 / fp16 only");
     if (!w || !out) return fail(RR_EINVAL, "rr_stem_pack_weights: null pointer");
     if (c_out != 64 || c_in != 3 || kh != 7 || kw != 7)
         return fail(RR_EINVAL, "rr_stem_pack_weights: the fused stem is the 3->64 7x7 conv1");
-    hipLaunchKernelGGL(k_stem_pack, dim3(64), dim3(256), 0, as_stream(stream), w, (bf16_t*)out);
+    if (dtype == RR_F16)
+        hipLaunchKernelGGL(k_stem_pack<f16_t>, dim3(64), dim3(256), 0, as_stream(stream), w, (f16_t*)out);
+    else
+        hipLaunchKernelGGL(k_stem_pack<bf16_t>, dim3(64), dim3(256), 0, as_stream(stream), w, (bf16_t*)out);
     return check_launch("rr_stem_pack_weights");
 }
 
 extern "C" int rr_stem_conv_pool(const float* x, int n, int h, int w, const float* mean_host, const float* std_host,
                                  int do_normalize, const void* wpk, const float* scale, const float* shift, int act,
-                                 float slope, void* y, int hp, int wp, void* stream) {
+                                 float slope, void* y, int hp, int wp, int dtype, void* stream) {
+    if (dtype != RR_BF16 && dtype != RR_F16) return fail(RR_EINVAL, "rr_stem_conv_pool: bf16 / fp16 only");
     if (!x || !wpk || !scale || !shift || !y) return fail(RR_EINVAL, "rr_stem_conv_pool: null pointer");
     if (n <= 0 || h <= 0 || w <= 0) return fail(RR_EINVAL, "rr_stem_conv_pool: bad shape");
     const int ho = (h + 2 * 3 - 7) / 2 + 1, wo = (w + 2 * 3 - 7) / 2 + 1;
@@ -282,7 +289,11 @@ extern "C" int rr_stem_conv_pool(const float* x, int n, int h, int w, const floa
     if (ntiles >= (1ll << 31)) return fail(RR_EINVAL, "rr_stem_conv_pool: too many tiles");
     const int g_stem_cus = grid_cus();
     const int grid = (int)(ntiles < g_stem_cus ? ntiles : g_stem_cus);
-    hipLaunchKernelGGL((k_stem_pool<PH, PW>), dim3(grid), dim3(NT), 0, as_stream(stream), a, tiles_w,
+    if (dtype == RR_F16)
+        hipLaunchKernelGGL((k_stem_pool<PH, PW, f16_t>), dim3(grid), dim3(NT), 0, as_stream(stream), a, tiles_w,
+                           tiles_w * tiles_h, (int)ntiles);
+    else
+        hipLaunchKernelGGL((k_stem_pool<PH, PW, bf16_t>), dim3(grid), dim3(NT), 0, as_stream(stream), a, tiles_w,
                        tiles_w * tiles_h, (int)ntiles);
     return check_launch("rr_stem_conv_pool");
 }

@@ -1,4 +1,6 @@
-// librr.so — streaming 1x1 conv for the HBM-bound bottleneck layers (bf16).
+// librr.so — streaming 1x1 conv for the HBM-bound bottleneck layers (bf16 or
+// fp16 operands: H16<H> picks the MFMA and the packing; 16-bit storage is
+// moved as raw bits).
 //
 // The 1x1 convolutions of a bottleneck (conv1 / conv3 / projection) have
 // K = 64..512: a few MFMAs per byte, so they are bound by HBM, not by the
@@ -25,7 +27,6 @@ namespace rr {
 
 namespace {
 
-typedef __attribute__((ext_vector_type(8))) __bf16 sbf16x8_t;
 typedef __attribute__((ext_vector_type(4))) float sf32x4_t;
 
 // LDS image of the weight slice: row r (packed output channel), 16-B chunk c
@@ -37,7 +38,7 @@ __device__ __forceinline__ int wswz(int row, int chunk) {
     return row * (K * 2) + ((chunk ^ f) << 4);
 }
 
-template <int TC, int K, int FN, int D, int NW, bool RES>
+template <int TC, int K, int FN, int D, int NW, bool RES, typename H>
 __global__ void __launch_bounds__(64 * NW) k_stream1x1(ConvArgs a, int nslices) {
     constexpr int NI = TC / 16;   // accumulator fragments (channels) per wave
     constexpr int NK = K / 32;    // MFMA K-steps
@@ -160,9 +161,7 @@ __global__ void __launch_bounds__(64 * NW) k_stream1x1(ConvArgs a, int nslices) 
                                               : *reinterpret_cast<const uint4*>(sA + abase + wswz<K>(ii * 16 + r16, kk * 4 + kq));
 #pragma unroll
                         for (int j = 0; j < FN; ++j)
-                            acc[h][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(sbf16x8_t, av),
-                                                                                __builtin_bit_cast(sbf16x8_t, bq[d][j][kk]),
-                                                                                acc[h][j], 0, 0, 0);
+                            acc[h][j] = H16<H>::mfma(av, bq[d][j][kk], acc[h][j]);
                     }
                 if (live) {
                     const int cl = 32 * i2 + 8 * kq;  // 8 consecutive channels of this lane
@@ -186,8 +185,8 @@ __global__ void __launch_bounds__(64 * NW) k_stream1x1(ConvArgs a, int nslices) 
                             const unsigned w4[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
                             for (int r = 0; r < 4; ++r) {
-                                v[2 * r] += __uint_as_float(w4[r] << 16);
-                                v[2 * r + 1] += __uint_as_float(w4[r] & 0xffff0000u);
+                                v[2 * r] += H16<H>::lo(w4[r]);
+                                v[2 * r + 1] += H16<H>::hi(w4[r]);
                             }
                         }
                         if (leaky) {
@@ -195,10 +194,10 @@ __global__ void __launch_bounds__(64 * NW) k_stream1x1(ConvArgs a, int nslices) 
                             for (int r = 0; r < 8; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * slope;
                         }
                         uint4 o;
-                        o.x = pack_bf16x2(v[0], v[1]);
-                        o.y = pack_bf16x2(v[2], v[3]);
-                        o.z = pack_bf16x2(v[4], v[5]);
-                        o.w = pack_bf16x2(v[6], v[7]);
+                        o.x = H16<H>::pack2(v[0], v[1]);
+                        o.y = H16<H>::pack2(v[2], v[3]);
+                        o.z = H16<H>::pack2(v[4], v[5]);
+                        o.w = H16<H>::pack2(v[6], v[7]);
                         if (p < P) *reinterpret_cast<uint4*>(Y + p * a.ldy + c0 + cl) = o;
                     }
                 }
@@ -241,7 +240,7 @@ struct PairArgs {
     float slope3, slope1;
 };
 
-template <int C1, int D, bool PROJ>
+template <int C1, int D, bool PROJ, typename H>
 __global__ void __launch_bounds__(512) k_stream_pair(PairArgs a) {
     constexpr int K3 = 64, C3 = 256, NW = 8;
     constexpr int NK3 = K3 / 32, NR3 = C3 / 32, NF1 = C1 / 16, NK1 = C3 / 32;
@@ -332,9 +331,7 @@ __global__ void __launch_bounds__(512) k_stream_pair(PairArgs a) {
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
                         const uint4 av = *reinterpret_cast<const uint4*>(sW3 + abase + wswz<K3>((2 * i2 + h) * 16 + r16, kk * 4 + kq));
-                        acc[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(sbf16x8_t, av),
-                                                                         __builtin_bit_cast(sbf16x8_t, bq[d][kk]),
-                                                                         acc[h], 0, 0, 0);
+                        acc[h] = H16<H>::mfma(av, bq[d][kk], acc[h]);
                     }
                 const int c = 32 * i2 + 8 * kq;
                 float v[8];
@@ -350,9 +347,7 @@ __global__ void __launch_bounds__(512) k_stream_pair(PairArgs a) {
 #pragma unroll
                         for (int h = 0; h < 2; ++h) {
                             const uint4 av = *reinterpret_cast<const uint4*>(sWp + abase + wswz<K3>((2 * i2 + h) * 16 + r16, kk * 4 + kq));
-                            pacc[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(sbf16x8_t, av),
-                                                                              __builtin_bit_cast(sbf16x8_t, rq[d][kk]),
-                                                                              pacc[h], 0, 0, 0);
+                            pacc[h] = H16<H>::mfma(av, rq[d][kk], pacc[h]);
                         }
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
@@ -364,18 +359,18 @@ __global__ void __launch_bounds__(512) k_stream_pair(PairArgs a) {
                     const unsigned w4[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        v[2 * r] += __uint_as_float(w4[r] << 16);
-                        v[2 * r + 1] += __uint_as_float(w4[r] & 0xffff0000u);
+                        v[2 * r] += H16<H>::lo(w4[r]);
+                        v[2 * r + 1] += H16<H>::hi(w4[r]);
                     }
                 }
                 if (leaky3) {
 #pragma unroll
                     for (int r = 0; r < 8; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * a.slope3;
                 }
-                yq[i2].x = pack_bf16x2(v[0], v[1]);
-                yq[i2].y = pack_bf16x2(v[2], v[3]);
-                yq[i2].z = pack_bf16x2(v[4], v[5]);
-                yq[i2].w = pack_bf16x2(v[6], v[7]);
+                yq[i2].x = H16<H>::pack2(v[0], v[1]);
+                yq[i2].y = H16<H>::pack2(v[2], v[3]);
+                yq[i2].z = H16<H>::pack2(v[4], v[5]);
+                yq[i2].w = H16<H>::pack2(v[6], v[7]);
                 if (st) *reinterpret_cast<uint4*>(a.y + p * C3 + c) = yq[i2];
             }
             load(d, strip_of(i + D));  // refill this slot: strip i + D
@@ -390,9 +385,7 @@ __global__ void __launch_bounds__(512) k_stream_pair(PairArgs a) {
 #pragma unroll
                 for (int o = 0; o < NF1; ++o) {
                     const uint4 av = *reinterpret_cast<const uint4*>(sW1 + abase + wswz<C3>(o * 16 + r16, kk * 4 + kq));
-                    zacc[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(sbf16x8_t, av),
-                                                                      __builtin_bit_cast(sbf16x8_t, yq[kk]), zacc[o],
-                                                                      0, 0, 0);
+                    zacc[o] = H16<H>::mfma(av, yq[kk], zacc[o]);
                 }
             }
 #pragma unroll
@@ -409,10 +402,10 @@ __global__ void __launch_bounds__(512) k_stream_pair(PairArgs a) {
                     for (int r = 0; r < 8; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * a.slope1;
                 }
                 uint4 o;
-                o.x = pack_bf16x2(v[0], v[1]);
-                o.y = pack_bf16x2(v[2], v[3]);
-                o.z = pack_bf16x2(v[4], v[5]);
-                o.w = pack_bf16x2(v[6], v[7]);
+                o.x = H16<H>::pack2(v[0], v[1]);
+                o.y = H16<H>::pack2(v[2], v[3]);
+                o.z = H16<H>::pack2(v[4], v[5]);
+                o.w = H16<H>::pack2(v[6], v[7]);
                 if (st) *reinterpret_cast<uint4*>(a.z + p * C1 + c) = o;
             }
         }
@@ -420,8 +413,8 @@ __global__ void __launch_bounds__(512) k_stream_pair(PairArgs a) {
 }
 
 
-template <int TC, int K, int FN, int D, int NW>
-void launch_s(const ConvArgs& a, hipStream_t s) {
+template <int TC, int K, int FN, int D, int NW, typename H>
+void launch_s_t(const ConvArgs& a, hipStream_t s) {
     const int g_stream_cus = grid_cus();
     constexpr int LDS = TC * K * 2 + TC * 8;
     constexpr int PER_CU = (160 * 1024 / LDS) >= 2 && NW <= 8 ? (NW <= 4 ? 4 : 2) : 1;
@@ -433,9 +426,9 @@ void launch_s(const ConvArgs& a, hipStream_t s) {
     if (per_slice > need) per_slice = need;
     const int grid = (int)(per_slice * nslices);
     if (a.flags & RR_CONV_RESIDUAL)
-        hipLaunchKernelGGL((k_stream1x1<TC, K, FN, D, NW, true>), dim3(grid), dim3(64 * NW), 0, s, a, nslices);
+        hipLaunchKernelGGL((k_stream1x1<TC, K, FN, D, NW, true, H>), dim3(grid), dim3(64 * NW), 0, s, a, nslices);
     else
-        hipLaunchKernelGGL((k_stream1x1<TC, K, FN, D, NW, false>), dim3(grid), dim3(64 * NW), 0, s, a, nslices);
+        hipLaunchKernelGGL((k_stream1x1<TC, K, FN, D, NW, false, H>), dim3(grid), dim3(64 * NW), 0, s, a, nslices);
 }
 
 }  // namespace
@@ -444,29 +437,35 @@ int g_stream_mode = 1;  // rr_set_tuning(RR_TUNE_STREAM_1X1): 0 off, 1 auto
 
 // bf16 1x1 (pad 0, any stride), PERM32 weights, bf16 out: returns false when the
 // shape is not one the streaming kernel is built for (caller uses the tiled engine).
-bool launch_stream1x1(const ConvArgs& a, hipStream_t s) {
+template <int TC, int K, int FN, int D, int NW>
+void launch_s(const ConvArgs& a, hipStream_t s, bool f16) {
+    if (f16) launch_s_t<TC, K, FN, D, NW, f16_t>(a, s);
+    else launch_s_t<TC, K, FN, D, NW, bf16_t>(a, s);
+}
+
+bool launch_stream1x1(const ConvArgs& a, hipStream_t s, bool f16) {
     if (g_stream_mode == 0) return false;
     if (!(a.flags & RR_CONV_PERM32) || a.kh != 1 || a.kw != 1 || a.pad != 0 || a.kp != a.cin) return false;
     if (a.P < 4096 || (long long)a.n * a.h * a.w_ * a.cin >= (1ll << 31)) return false;
     const bool res = a.flags & RR_CONV_RESIDUAL;
     const int K = a.cin, C = a.cout;
-    if (K == 64 && C == 64) { launch_s<64, 64, 2, 4, 8>(a, s); return true; }
-    if (K == 64 && C == 256) { launch_s<256, 64, 1, 2, 8>(a, s); return true; }
-    if (K == 256 && C == 64) { launch_s<64, 256, 1, 4, 8>(a, s); return true; }
-    if (K == 256 && C == 128) { launch_s<128, 256, 1, 3, 8>(a, s); return true; }
-    if (K == 128 && C == 512) { launch_s<256, 128, 1, 3, 8>(a, s); return true; }
-    if (K == 512 && C == 128) { launch_s<128, 512, 1, 2, 8>(a, s); return true; }
-    if (K == 256 && C == 1024 && res) { launch_s<256, 256, 1, 2, 8>(a, s); return true; }
-    if (K == 256 && C == 512 && !res) { launch_s<256, 256, 1, 2, 8>(a, s); return true; }
+    if (K == 64 && C == 64) { launch_s<64, 64, 2, 4, 8>(a, s, f16); return true; }
+    if (K == 64 && C == 256) { launch_s<256, 64, 1, 2, 8>(a, s, f16); return true; }
+    if (K == 256 && C == 64) { launch_s<64, 256, 1, 4, 8>(a, s, f16); return true; }
+    if (K == 256 && C == 128) { launch_s<128, 256, 1, 3, 8>(a, s, f16); return true; }
+    if (K == 128 && C == 512) { launch_s<256, 128, 1, 3, 8>(a, s, f16); return true; }
+    if (K == 512 && C == 128) { launch_s<128, 512, 1, 2, 8>(a, s, f16); return true; }
+    if (K == 256 && C == 1024 && res) { launch_s<256, 256, 1, 2, 8>(a, s, f16); return true; }
+    if (K == 256 && C == 512 && !res) { launch_s<256, 256, 1, 2, 8>(a, s, f16); return true; }
     // 128-channel slices of a 512-deep panel: the input is re-read per slice
     // (from L2 / Infinity Cache: slices of one strip run side by side), the
     // output and residual stream once (mod5 conv3 461 -> 600, mod4 conv1
     // 606 -> 673, mod4 projection 632 -> 695 TFLOP/s at 128 images vs the
     // tiled engine).  K = 1024 does not fit: one strip's B operand alone is
     // 128 VGPRs, and a single-strip-deep stream measured 395-410 vs 712-720.
-    if (K == 512 && C == 2048 && res) { launch_s<128, 512, 1, 2, 8>(a, s); return true; }
-    if (K == 512 && C == 256 && !res) { launch_s<128, 512, 1, 2, 8>(a, s); return true; }
-    if (K == 512 && C == 1024 && !res) { launch_s<128, 512, 1, 2, 8>(a, s); return true; }
+    if (K == 512 && C == 2048 && res) { launch_s<128, 512, 1, 2, 8>(a, s, f16); return true; }
+    if (K == 512 && C == 256 && !res) { launch_s<128, 512, 1, 2, 8>(a, s, f16); return true; }
+    if (K == 512 && C == 1024 && !res) { launch_s<128, 512, 1, 2, 8>(a, s, f16); return true; }
     return false;
 }
 
@@ -480,7 +479,7 @@ extern "C" int rr_conv1x1_pair(const void* x, long long p, int c_in, const void*
                                const float* scalep, const float* shiftp, int act3, float slope3, const void* w1,
                                const float* scale1, const float* shift1, int c_out, int act1, float slope1, void* y,
                                void* z, int dtype, void* stream) {
-    if (dtype != RR_BF16) return fail(RR_EINVAL, "rr_conv1x1_pair: bf16 only");
+    if (dtype != RR_BF16 && dtype != RR_F16) return fail(RR_EINVAL, "rr_conv1x1_pair: bf16 / fp16 only");
     if (c_in != 64 || c_mid != 256 || (c_out != 64 && c_out != 128))
         return fail(RR_EINVAL, "rr_conv1x1_pair: shapes (c_in 64, c_mid 256, c_out 64|128) only");
     if (!x || !w3 || !scale3 || !shift3 || !w1 || !scale1 || !shift1 || !y || !z)
@@ -507,9 +506,14 @@ extern "C" int rr_conv1x1_pair(const void* x, long long p, int c_in, const void*
     if (grid > g_pair_cus) grid = g_pair_cus;
     const dim3 g((unsigned)grid), b(512);
     hipStream_t s = as_stream(stream);
-    if (c_out == 64 && !proj) hipLaunchKernelGGL((k_stream_pair<64, 2, false>), g, b, 0, s, a);
-    else if (c_out == 64) hipLaunchKernelGGL((k_stream_pair<64, 2, true>), g, b, 0, s, a);
-    else if (!proj) hipLaunchKernelGGL((k_stream_pair<128, 2, false>), g, b, 0, s, a);
-    else hipLaunchKernelGGL((k_stream_pair<128, 2, true>), g, b, 0, s, a);
+    auto go = [&](auto h) {
+        using H = decltype(h);
+        if (c_out == 64 && !proj) hipLaunchKernelGGL((k_stream_pair<64, 2, false, H>), g, b, 0, s, a);
+        else if (c_out == 64) hipLaunchKernelGGL((k_stream_pair<64, 2, true, H>), g, b, 0, s, a);
+        else if (!proj) hipLaunchKernelGGL((k_stream_pair<128, 2, false, H>), g, b, 0, s, a);
+        else hipLaunchKernelGGL((k_stream_pair<128, 2, true, H>), g, b, 0, s, a);
+    };
+    if (dtype == RR_F16) go(f16_t{});
+    else go(bf16_t{});
     return check_launch("rr_conv1x1_pair");
 }

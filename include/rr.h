@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-enum rr_dtype { RR_F32 = 0, RR_BF16 = 1, RR_F16 = 2 };  /* RR_F16: kNN screening + the generic conv engine (natural-order weights) */
+enum rr_dtype { RR_F32 = 0, RR_BF16 = 1, RR_F16 = 2 };  /* 16-bit types: every conv kernel; RR_F16 also kNN screening */
 enum rr_act { RR_ACT_IDENTITY = 0, RR_ACT_LEAKY = 1 };
 enum rr_pool_mode { RR_POOL_GEM = 0, RR_POOL_MAC = 1, RR_POOL_SPOC = 2 };
 enum rr_conv_flags { RR_CONV_AFFINE = 1, RR_CONV_RESIDUAL = 2, RR_CONV_PERM32 = 4 };
@@ -91,7 +91,7 @@ int rr_conv2d_fused(const void* x, const void* w, const float* scale, const floa
 int rr_pack_conv_weights(const float* w, int c_out, int c_in, int kh, int kw, int c_in_pad,
                          int k_packed, int perm32, void* out, int dtype, void* stream);
 
-/* Fused bottleneck boundary, bf16, PERM32-packed weights (1x1 convs):
+/* Fused bottleneck boundary, bf16 or fp16 (dtype), PERM32-packed weights (1x1 convs):
  *   y = act3(conv1x1(x, w3) * scale3 + shift3 + shortcut)      [p][c_mid]
  *   z = act1(conv1x1(y, w1) * scale1 + shift1)                 [p][c_out]
  * i.e. conv3 + bn3 + residual add + activation of ResidualBlock i and conv1 +
@@ -113,18 +113,18 @@ int rr_conv1x1_pair(const void* x, long long p, int c_in, const void* w3, const 
 int rr_maxpool2d(const void* x, int n, int h, int w, int c, int k, int stride, int pad,
                  void* y, int ho, int wo, int dtype, void* stream);
 
-/* Fused ResNet stem, bf16: normalise + conv1 7x7/s2/p3 (3 -> 64) + BN affine
+/* Fused ResNet stem, bf16 or fp16 (dtype): normalise + conv1 7x7/s2/p3 (3 -> 64) + BN affine
  * + activation + max-pool 3x3/s2/p1 in one kernel.  Replaces mod1 =
  * Sequential(conv1, bn1, pool1) of cirtorch/backbones/resnet.py:59-66 applied
  * to the output of utils/image.py:125 `normalize`.
  *   x     : [n][3][h][w] float32 (raw pixels when do_normalize, mean/std HOST arrays of 3)
- *   wpk   : rr_stem_pack_weights output, bf16 [64][256]
+ *   wpk   : rr_stem_pack_weights output, [64][256] (dtype)
  *   scale, shift : [64] float32 (folded BN), act RR_ACT_*, slope for leaky
- *   y     : [n][hp][wp][64] bf16, hp/wp = the pool of the (h+1)/2 x (w+1)/2 stem map */
-int rr_stem_pack_weights(const float* w, int c_out, int c_in, int kh, int kw, void* out, void* stream);
+ *   y     : [n][hp][wp][64] (dtype), hp/wp = the pool of the (h+1)/2 x (w+1)/2 stem map */
+int rr_stem_pack_weights(const float* w, int c_out, int c_in, int kh, int kw, void* out, int dtype, void* stream);
 int rr_stem_conv_pool(const float* x, int n, int h, int w, const float* mean_host, const float* std_host,
                       int do_normalize, const void* wpk, const float* scale, const float* shift, int act,
-                      float slope, void* y, int hp, int wp, void* stream);
+                      float slope, void* y, int hp, int wp, int dtype, void* stream);
 
 /* Bilinear resize, align_corners=False, NCHW float32 (one image).
  * Replaces nn.functional.interpolate(scale_factor=s, mode='bilinear',

@@ -78,14 +78,14 @@ STREAM_CASES = [
 
 
 @pytest.mark.parametrize("case", STREAM_CASES)
-@pytest.mark.parametrize("mode", [1, 0])
-def test_conv_stream1x1(cuda, case, mode):
+@pytest.mark.parametrize("mode,prec", [(1, "bf16"), (0, "bf16"), (1, "fp16")])
+def test_conv_stream1x1(cuda, case, mode, prec):
     """The weight-stationary streaming 1x1 kernel (mode 1) and the tiled engine
     (mode 0) on the same shapes."""
     from cirtorch import _engine as E
     E.check(E.lib().rr_set_tuning(5, mode), "rr_set_tuning")
     try:
-        _check_conv(cuda, case, "bf16", True)
+        _check_conv(cuda, case, prec, True)
     finally:
         E.lib().rr_set_tuning(5, 1)
 
@@ -102,14 +102,15 @@ CONV3_CASES = [
 
 
 @pytest.mark.parametrize("case", CONV3_CASES)
-@pytest.mark.parametrize("mode", [1, 2, 3, 4, 6, 7, 8, 0])
-def test_conv3x3_direct(cuda, case, mode):
+@pytest.mark.parametrize("mode,prec", [(1, "bf16"), (2, "bf16"), (3, "bf16"), (4, "bf16"), (6, "bf16"), (7, "bf16"),
+                                       (8, "bf16"), (0, "bf16"), (1, "fp16"), (8, "fp16"), (0, "fp16")])
+def test_conv3x3_direct(cuda, case, mode, prec):
     """Direct 3x3 kernel (modes 1-4, 6: auto / 8x32 / 4x32 tiles / A-stationary wave layouts) and the
     implicit-GEMM fallback (mode 0) against the float64 reference."""
     from cirtorch import _engine as E
     E.check(E.lib().rr_set_tuning(6, mode), "rr_set_tuning")
     try:
-        _check_conv(cuda, case, "bf16", True)
+        _check_conv(cuda, case, prec, True)
     finally:
         E.lib().rr_set_tuning(6, 1)
 
@@ -235,33 +236,35 @@ def test_whitenapply_vs_reference_golden(cuda):
 
 @pytest.mark.parametrize("shape", [(2, 61, 83), (1, 96, 128), (1, 40, 300)])
 @pytest.mark.parametrize("norm", [True, False])
-def test_stem_conv_pool(cuda, shape, norm):
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_stem_conv_pool(cuda, dt, shape, norm):
     """Fused normalise + conv1 7x7/s2/p3 + BN + leaky + maxpool 3x3/s2/p1
     (cirtorch/backbones/resnet.py:59-66) against an fp64 restatement on the
     same bf16-rounded operands, and against the unfused engine path."""
+    rnd = lambda t: t.to(dt).float()  # noqa: E731
     n, h, w = shape
     g = torch.Generator().manual_seed(h * 1000 + w)
     x = torch.rand(n, 3, h, w, generator=g)
-    wt = _bf16_round(torch.randn(64, 3, 7, 7, generator=g) * 0.1)
+    wt = rnd(torch.randn(64, 3, 7, 7, generator=g) * 0.1)
     scale = torch.rand(64, generator=g) + 0.5
     shift = torch.randn(64, generator=g) * 0.1
     mean, std = ([0.485, 0.456, 0.406], [0.229, 0.224, 0.225]) if norm else (None, None)
     ops = _ops()
-    wpk = ops.pack_stem_weights(wt.to(cuda))
+    wpk = ops.pack_stem_weights(wt.to(cuda), dt)
     got = ops.stem_conv_pool(x.to(cuda), wpk, scale.to(cuda), shift.to(cuda), leaky=True, slope=0.01,
                              mean=mean, std=std).float().cpu()
     xn = x if not norm else (x - torch.tensor(mean)[:, None, None]) / torch.tensor(std)[:, None, None]
-    xn = _bf16_round(xn)
+    xn = rnd(xn)
     ref = F.conv2d(xn.double(), wt.double(), stride=2, padding=3) * scale.double()[None, :, None, None] \
         + shift.double()[None, :, None, None]
-    ref = _bf16_round(F.leaky_relu(ref, 0.01).float())
+    ref = rnd(F.leaky_relu(ref, 0.01).float())
     ref = F.max_pool2d(ref, 3, 2, 1).permute(0, 2, 3, 1)
     assert got.shape == ref.shape
     err = (got - ref).abs().max().item()
     assert err <= 8e-3 * ref.abs().max().item(), err
     # unfused engine path on the same inputs
-    xe = ops.image_to_nhwc(x.to(cuda), 8, torch.bfloat16, mean, std)
-    wp = ops.pack_conv_weights(wt.to(cuda), 8, torch.bfloat16, perm32=True)
+    xe = ops.image_to_nhwc(x.to(cuda), 8, dt, mean, std)
+    wp = ops.pack_conv_weights(wt.to(cuda), 8, dt, perm32=True)
     y = ops.conv2d_fused(xe, wp, 7, 7, 2, 3, 64, scale.to(cuda), shift.to(cuda), leaky=True, perm32=True)
     un = ops.maxpool2d(y, 3, 2, 1).float().cpu()
     assert (got - un).abs().max().item() <= 8e-3 * ref.abs().max().item()
@@ -271,27 +274,29 @@ def test_stem_conv_pool(cuda, shape, norm):
 
 @pytest.mark.parametrize("c_out", [64, 128])
 @pytest.mark.parametrize("shape", [(2, 23, 37), (1, 64, 96)])
-def test_conv1x1_pair(cuda, c_out, shape):
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_conv1x1_pair(cuda, dt, c_out, shape):
     """Fused bottleneck boundary (rr_conv1x1_pair): conv3 (64->256) + BN +
     residual + leaky of block i and conv1 (256->c_out) + BN + leaky of block
     i+1 (cirtorch/backbones/misc.py:166-203) vs a float64 restatement, and vs
     the two separate engine launches (same bf16 roundings, so bit-identical
     up to fp32 summation order)."""
+    rnd = lambda t: t.to(dt).float()  # noqa: E731
     n, h, w = shape
     g = torch.Generator().manual_seed(c_out * 7 + h)
     ops = _ops()
-    x = _bf16_round(torch.randn(n, 64, h, w, generator=g))
-    w3 = _bf16_round(torch.randn(256, 64, 1, 1, generator=g) * (2.0 / 64) ** 0.5)
-    w1 = _bf16_round(torch.randn(c_out, 256, 1, 1, generator=g) * (2.0 / 256) ** 0.5)
+    x = rnd(torch.randn(n, 64, h, w, generator=g))
+    w3 = rnd(torch.randn(256, 64, 1, 1, generator=g) * (2.0 / 64) ** 0.5)
+    w1 = rnd(torch.randn(c_out, 256, 1, 1, generator=g) * (2.0 / 256) ** 0.5)
     s3, h3 = torch.rand(256, generator=g) + 0.5, torch.randn(256, generator=g) * 0.1
     s1, h1 = torch.rand(c_out, generator=g) + 0.5, torch.randn(c_out, generator=g) * 0.1
-    res = _bf16_round(torch.randn(n, 256, h, w, generator=g))
+    res = rnd(torch.randn(n, 256, h, w, generator=g))
     yr = F.leaky_relu(F.conv2d(x.double(), w3.double()) * s3.double()[None, :, None, None]
                       + h3.double()[None, :, None, None] + res.double(), 0.01)
-    yb = _bf16_round(yr.float()).double()
+    yb = rnd(yr.float()).double()
     zr = F.leaky_relu(F.conv2d(yb, w1.double()) * s1.double()[None, :, None, None] + h1.double()[None, :, None, None],
                       0.01)
-    bf = torch.bfloat16
+    bf = dt
     xe = x.permute(0, 2, 3, 1).contiguous().to(bf).to(cuda)
     re = res.permute(0, 2, 3, 1).contiguous().to(bf).to(cuda)
     w3p = ops.pack_conv_weights(w3.to(cuda), 64, bf, perm32=True)
@@ -310,17 +315,19 @@ def test_conv1x1_pair(cuda, c_out, shape):
 
 
 @pytest.mark.parametrize("c_out", [64, 128])
-def test_conv1x1_pair_projection(cuda, c_out):
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_conv1x1_pair_projection(cuda, dt, c_out):
     """First block of the stage: the shortcut is proj_bn(proj_conv(x_in))
     (cirtorch/backbones/misc.py:179-182), computed inside the fused launch."""
+    rnd = lambda t: t.to(dt).float()  # noqa: E731
     n, h, w = 2, 19, 29
     g = torch.Generator().manual_seed(c_out + 3)
     ops = _ops()
-    x = _bf16_round(torch.randn(n, 64, h, w, generator=g))
-    xin = _bf16_round(torch.randn(n, 64, h, w, generator=g))
-    w3 = _bf16_round(torch.randn(256, 64, 1, 1, generator=g) * (2.0 / 64) ** 0.5)
-    wpj = _bf16_round(torch.randn(256, 64, 1, 1, generator=g) * (2.0 / 64) ** 0.5)
-    w1 = _bf16_round(torch.randn(c_out, 256, 1, 1, generator=g) * (2.0 / 256) ** 0.5)
+    x = rnd(torch.randn(n, 64, h, w, generator=g))
+    xin = rnd(torch.randn(n, 64, h, w, generator=g))
+    w3 = rnd(torch.randn(256, 64, 1, 1, generator=g) * (2.0 / 64) ** 0.5)
+    wpj = rnd(torch.randn(256, 64, 1, 1, generator=g) * (2.0 / 64) ** 0.5)
+    w1 = rnd(torch.randn(c_out, 256, 1, 1, generator=g) * (2.0 / 256) ** 0.5)
     s3, h3 = torch.rand(256, generator=g) + 0.5, torch.randn(256, generator=g) * 0.1
     sp, hp = torch.rand(256, generator=g) + 0.5, torch.randn(256, generator=g) * 0.1
     s1, h1 = torch.rand(c_out, generator=g) + 0.5, torch.randn(c_out, generator=g) * 0.1
@@ -329,12 +336,12 @@ def test_conv1x1_pair_projection(cuda, c_out):
         return v.double()[None, :, None, None]
 
     def nhwc(t):
-        return t.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(cuda)
+        return t.permute(0, 2, 3, 1).contiguous().to(dt).to(cuda)
 
     short = F.conv2d(xin.double(), wpj.double()) * col(sp) + col(hp)
     yr = F.leaky_relu(F.conv2d(x.double(), w3.double()) * col(s3) + col(h3) + short, 0.01)
-    zr = F.leaky_relu(F.conv2d(_bf16_round(yr.float()).double(), w1.double()) * col(s1) + col(h1), 0.01)
-    bf = torch.bfloat16
+    zr = F.leaky_relu(F.conv2d(rnd(yr.float()).double(), w1.double()) * col(s1) + col(h1), 0.01)
+    bf = dt
     w3p = ops.pack_conv_weights(w3.to(cuda), 64, bf, perm32=True)
     wpp = ops.pack_conv_weights(wpj.to(cuda), 64, bf, perm32=True)
     w1p = ops.pack_conv_weights(w1.to(cuda), 256, bf, perm32=True)
@@ -347,8 +354,8 @@ def test_conv1x1_pair_projection(cuda, c_out):
 
 
 FP16_CASES = [
-    # the generic LDS-DMA engine in fp16 (natural-order weights): 1x1, strided 1x1,
-    # 3x3 s1/s2, the 7x7/s2 stem shape on 8 padded channels, residual + leaky
+    # the LDS-DMA engine in fp16 (natural-order weights): 1x1, strided 1x1, 3x3
+    # s1/s2, the 7x7/s2 stem shape on 8 padded channels, residual + leaky
     (2, 64, 17, 23, 256, 1, 1, 0, True, True),
     (2, 256, 18, 22, 512, 1, 2, 0, False, False),
     (2, 64, 16, 32, 64, 3, 1, 1, False, True),
@@ -378,14 +385,3 @@ def test_conv_fp16_splits_large_batches(cuda):
         yi = _ops().conv2d_fused(x[i:i + 1].contiguous(), wp, 1, 1, 1, 0, 64, leaky=False)
         assert torch.equal(y[i:i + 1], yi)
     del x
-
-
-def test_conv_fp16_rejects_perm32(cuda):
-    import ctypes
-    from cirtorch import _engine as E
-    x = torch.zeros(1, 4, 4, 64, dtype=torch.float16, device=cuda)
-    w = torch.zeros(64, 64, dtype=torch.float16, device=cuda)
-    y = torch.empty(16, 64, dtype=torch.float16, device=cuda)
-    d = E.ConvDesc(1, 4, 4, 64, 4, 4, 64, 1, 1, 1, 0, 1, 64, 64, 0, 0.0, E.RR_CONV_PERM32)
-    rc = E.lib().rr_conv2d_fused(E.ptr(x), E.ptr(w), None, None, None, E.ptr(y), ctypes.byref(d), 2, 2, None)
-    assert rc == -1 and b"PERM32" in E.lib().rr_last_error()
