@@ -301,7 +301,7 @@ def local_head(x, kpts, weight, bias):
     xh = x.permute(0, 2, 3, 1)
     if not xh.is_contiguous():
         xh = xh.contiguous()
-    if xh.dtype not in (torch.float32, torch.bfloat16):
+    if xh.dtype not in (torch.float32, torch.bfloat16, torch.float16):
         xh = xh.float()
     kp = kpts.contiguous().float()
     npts = kp.shape[1]

@@ -7,7 +7,7 @@
 // and the mutual-nearest-neighbour check of the HPatches matcher
 // (cirtorch/utils/evaluation/HPatchesEval.py:31-43) on top of rr_knn_topk.
 //
-// Layout: feature map NHWC (any of the extractor's stage maps, bf16 or f32),
+// Layout: feature map NHWC (any of the extractor's stage maps, bf16/fp16/f32),
 // keypoints [n][npts][2] float32 in grid_sample's normalised (x, y) in [-1, 1].
 // Sampling: one wave per keypoint, lanes over channels (16-B loads of 8 bf16 /
 // 4 f32 channels), the four bilinear taps in torch's order (nw, ne, sw, se),
@@ -30,6 +30,15 @@ template <> struct LVec<bf16_t> {
             v[2 * e] = __uint_as_float(w[e] << 16);
             v[2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
         }
+    }
+};
+template <> struct LVec<f16_t> {
+    static constexpr int N = 8;
+    static __device__ __forceinline__ void load(const f16_t* p, float* v) {
+        typedef __attribute__((ext_vector_type(8))) _Float16 h8;
+        const h8 q = *reinterpret_cast<const h8*>(p);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (float)q[e];
     }
 };
 template <> struct LVec<float> {
@@ -136,8 +145,8 @@ int rr_local_head(const void* x, int n, int h, int w, int c, int dtype, const fl
                   size_t workspace_bytes, void* stream) {
     if (!x || !kpts || !weight || !out) return fail(RR_EINVAL, "rr_local_head: null pointer");
     if (n <= 0 || h <= 0 || w <= 0 || c <= 0 || npts <= 0 || e <= 0) return fail(RR_EINVAL, "rr_local_head: empty");
-    const int vec = dtype == RR_BF16 ? 8 : 4;
-    if (dtype != RR_BF16 && dtype != RR_F32) return fail(RR_EINVAL, "rr_local_head: dtype");
+    const int vec = dtype == RR_F32 ? 4 : 8;
+    if (dtype != RR_BF16 && dtype != RR_F16 && dtype != RR_F32) return fail(RR_EINVAL, "rr_local_head: dtype");
     if (c % vec || (((uintptr_t)x) & 15)) return fail(RR_EINVAL, "rr_local_head: c must fill 16-byte lanes");
     if (c % 4) return fail(RR_EINVAL, "rr_local_head: c % 4 != 0");
     const long long nkp = (long long)n * npts;
@@ -150,6 +159,9 @@ int rr_local_head(const void* x, int n, int h, int w, int c, int dtype, const fl
     const unsigned g = (unsigned)((nkp + 3) / 4);
     if (dtype == RR_BF16)
         hipLaunchKernelGGL(k_grid_sample_nhwc<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)x, h, w, c, kpts, npts,
+                           nkp, samp);
+    else if (dtype == RR_F16)
+        hipLaunchKernelGGL(k_grid_sample_nhwc<f16_t>, dim3(g), dim3(256), 0, s, (const f16_t*)x, h, w, c, kpts, npts,
                            nkp, samp);
     else
         hipLaunchKernelGGL(k_grid_sample_nhwc<float>, dim3(g), dim3(256), 0, s, (const float*)x, h, w, c, kpts, npts,

@@ -27,12 +27,13 @@ def test_local_head_vs_reference_golden(cuda, tag, layout):
     np.testing.assert_allclose(got, g["desc_" + tag], rtol=0, atol=2e-6)
 
 
-def test_local_head_bf16_map(cuda):
-    """bf16 stage map (the engine's extractor output dtype): descriptors within bf16 input rounding."""
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_local_head_16bit_map(cuda, dt):
+    """bf16 / fp16 stage map (the engine's extractor output dtypes): descriptors within input rounding."""
     from cirtorch import _ops
     g = golden("local.npz")
     x = torch.from_numpy(g["x_b"])
-    xb = x.to(torch.bfloat16)
+    xb = x.to(dt)
     ref = torch.from_numpy(g["desc_b"])
     from oracle import ops
     ref_b = ops.local_head(xb.float(), torch.from_numpy(g["kpts_b"]), torch.from_numpy(g["w_b"]),
