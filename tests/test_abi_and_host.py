@@ -160,3 +160,17 @@ def test_whitenlearn_host_matches_reference_golden():
     m, P = whitenlearn(X, g["qidxs"], g["pidxs"])
     np.testing.assert_allclose(m, g["m"], rtol=1e-12)
     np.testing.assert_allclose(np.abs(P), np.abs(g["P"]), rtol=1e-6, atol=1e-8)
+
+
+def test_pmc_traffic_profile_matches_bench_defaults():
+    """bench.py reports roofline.traffic only when profiles/r01_pmc_traffic.json
+    was measured on its default workload; keep the file's config keys in step."""
+    import json
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    t = json.load(open(os.path.join(root, "profiles", "r01_pmc_traffic.json")))
+    c = t["config"]
+    assert (c["arch"], c["precision"], c["image"]) == ("resnet50", "bf16", [3, 768, 1024])
+    assert c["batch"] == 128 and c.get("source_commit")
+    # measured HBM bytes per image >= the algorithmic 808 MB of the body's layers
+    assert 8.0e8 < t["hbm_bytes_per_image"] < 1.2e9
