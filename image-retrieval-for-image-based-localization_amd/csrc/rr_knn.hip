@@ -6,7 +6,9 @@
 // Pipeline per query batch (all on one HIP stream, no host sync):
 //  1. score GEMM   slab[q][n] = <q, db_n> for a pass of G chunks of L rows,
 //                  MFMA (bf16 or exact f32), f32 scores.  The slab is sized to
-//                  stay resident in the 256 MiB Infinity Cache (<= 64 MiB).
+//                  at most 512 MiB per pass: fewer, fuller GEMM tile loops
+//                  (Q = 128 over 1M rows: 64 / 256 / 512 MiB -> 1.71 / 1.53 /
+//                  1.49 ms; Q = 1024: 8.27 / 7.62 / 7.44 ms).
 //  2. chunk select per (query, chunk): radix-select of the top KC fp32 keys
 //                  over L scores staged in LDS; candidates emitted in index
 //                  order (deterministic, ties -> lower index).
@@ -19,13 +21,24 @@
 // ~1e-7, far below KC-k candidates' worth of score density at the boundary.
 #include "rr_internal.h"
 
+#include <cstdlib>
+
 namespace rr {
 
 
 constexpr int SEL_THREADS = 1024;
 constexpr int SEL_WAVES = SEL_THREADS / 64;
 constexpr int CHUNK_L = 16384;           // rows per select chunk (keys staged in 64 KiB LDS)
-constexpr size_t SLAB_BUDGET = 64ull << 20;
+// score-slab budget per GEMM pass (Infinity-Cache resident); RR_KNN_SLAB_MB overrides (tuning)
+static size_t slab_budget() {
+    static size_t b = 0;
+    if (!b) {
+        const char* e = getenv("RR_KNN_SLAB_MB");
+        const long v = e ? atol(e) : 0;
+        b = (v >= 16 && v <= 1024) ? (size_t)v << 20 : (512ull << 20);
+    }
+    return b;
+}
 constexpr int MAX_SORT = 8192;
 constexpr int TOPK_BINS = 2048;          // radix-select histogram (11-bit digits)
 
@@ -40,15 +53,22 @@ __device__ __forceinline__ float funkey(uint32_t k) {
 // Top-K (largest keys) of keys[0..len) with index-order ties.  `getk(i)` gives
 // the key, `geti(i)` the payload index; K results are written to out_k/out_i
 // in ascending position order; missing slots get (key 0, index -1).
-template <typename GK, typename GI>
-__device__ void block_topk(GK getk, GI geti, int len, int K, uint32_t* out_k, int* out_i, int* smem_i) {
+// SKIP0: key 0 marks a slot screened out before the select (below the query's
+// running threshold); such keys are neither counted nor emitted, `nvalid` is
+// the number of non-zero keys, and fewer than K of them are emitted in index
+// order followed by (0, -1) padding.  Returns the K-th key (0 when every valid
+// key was taken).
+template <bool SKIP0 = false, typename GK, typename GI>
+__device__ uint32_t block_topk(GK getk, GI geti, int len, int K, uint32_t* out_k, int* out_i, int* smem_i,
+                               int nvalid = -1) {
+    if (!SKIP0) nvalid = len;
     int* hist = smem_i;                        // TOPK_BINS
     int* wsum = smem_i + TOPK_BINS;            // SEL_WAVES + 1
     int* sel = smem_i + TOPK_BINS + 32;        // [0]=digit, [1]=remaining
     const int tid = threadIdx.x;
     uint32_t thr = 0;
     int remaining = K;
-    if (len > K) {
+    if (nvalid > K) {
         // digits of 11, 11 and 10 bits: the first covers sign, exponent and two
         // mantissa bits, so the scores' few exponents spread over many bins
         // (fewer same-address LDS atomics than an 8-bit top digit), 3 passes.
@@ -61,7 +81,7 @@ __device__ void block_topk(GK getk, GI geti, int len, int K, uint32_t* out_k, in
             __syncthreads();
             for (int i = tid; i < len; i += SEL_THREADS) {
                 uint32_t k = getk(i);
-                if ((k & mask) == prefix) atomicAdd(&hist[(k >> shift) & dmask], 1);
+                if ((k & mask) == prefix && (!SKIP0 || k != 0u)) atomicAdd(&hist[(k >> shift) & dmask], 1);
             }
             __syncthreads();
             if (tid < 64) {
@@ -106,7 +126,7 @@ __device__ void block_topk(GK getk, GI geti, int len, int K, uint32_t* out_k, in
     const int lane = tid & 63, w = tid >> 6;
     int* wgt = wsum;                 // SEL_WAVES counts of keys above the threshold
     int* weq = smem_i + TOPK_BINS + 40;  // SEL_WAVES counts of keys equal to it
-    const bool sel_all = len <= K;
+    const bool sel_all = nvalid <= K;
     const int wseg = (((len + SEL_WAVES - 1) / SEL_WAVES) + 63) & ~63;
     const int wb = min(len, w * wseg), we = min(len, wb + wseg);
     int cgt = 0, ceq = 0;
@@ -114,7 +134,7 @@ __device__ void block_topk(GK getk, GI geti, int len, int K, uint32_t* out_k, in
         const int i = i0 + lane;
         const bool in = i < we;
         const uint32_t k = in ? getk(i) : 0u;
-        cgt += __popcll(__ballot(in && (sel_all || k > thr)));
+        cgt += __popcll(__ballot(in && (sel_all ? (!SKIP0 || k != 0u) : k > thr)));
         ceq += __popcll(__ballot(in && !sel_all && k == thr));
     }
     if (lane == 0) {
@@ -131,7 +151,7 @@ __device__ void block_topk(GK getk, GI geti, int len, int K, uint32_t* out_k, in
         const int i = i0 + lane;
         const bool in = i < we;
         const uint32_t k = in ? getk(i) : 0u;
-        const bool gt = in && (sel_all || k > thr);
+        const bool gt = in && (sel_all ? (!SKIP0 || k != 0u) : k > thr);
         const bool eq = in && !sel_all && k == thr;
         const unsigned long long bg = __ballot(gt), be = __ballot(eq);
         const int rg = pgt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bg >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bg, 0u));
@@ -148,37 +168,83 @@ __device__ void block_topk(GK getk, GI geti, int len, int K, uint32_t* out_k, in
         peq += __popcll(be);
     }
     if (sel_all) {
-        for (int i = len + tid; i < K; i += SEL_THREADS) {
+        for (int i = nvalid + tid; i < K; i += SEL_THREADS) {
             out_k[i] = 0u;
             out_i[i] = -1;
         }
     }
     __syncthreads();
+    return thr;
 }
 
 // ---------------------------------------------------------------- chunk select
 // grid (nq, chunks in pass).  slab row q: slab + q*S; chunk c covers
 // columns [c*L, c*L + len).  Global row index of column j = row0 + c*L + j.
+// tau[q]: the query's running screen threshold = the largest K-th key any
+// earlier (or concurrent) chunk of this search has selected.  Keys below it
+// cannot reach the final top KC — that chunk already put KC keys >= tau into
+// the candidate pool — so they are dropped at load time (key 0): the radix
+// passes skip them and a chunk with <= KC survivors skips the passes
+// altogether.  The final select's result is unchanged by construction:
+// every candidate removed is below KC pool keys, and the kept ones keep their
+// index order.  Reads of tau race benignly with other chunks' atomicMax (any
+// value ever stored is a valid bound).
 __global__ void __launch_bounds__(SEL_THREADS) k_chunk_select(const float* __restrict__ slab, long long S, int L,
                                                               int rows_in_pass, int row0, int chunk0, int nchunks,
                                                               int KC, uint32_t* __restrict__ cand_k,
-                                                              int* __restrict__ cand_i) {
+                                                              int* __restrict__ cand_i, uint32_t* tau) {
     extern __shared__ __attribute__((aligned(16))) uint32_t keys[];  // L
     __shared__ int smi[TOPK_BINS + 64];
+    __shared__ int nsurv;
     const int q = blockIdx.x, c = blockIdx.y;
     const int len = min(L, rows_in_pass - c * L);
     const float* src = slab + (long long)q * S + (long long)c * L;
-    // slab rows start 16-B aligned (S % 4 == 0, L % 4 == 0): float4 loads
-    const int len4 = len & ~3;
-    for (int i = threadIdx.x * 4; i < len4; i += SEL_THREADS * 4) {
-        const float4 v = *reinterpret_cast<const float4*>(src + i);
-        *reinterpret_cast<uint4*>(keys + i) = make_uint4(fkey(v.x), fkey(v.y), fkey(v.z), fkey(v.w));
-    }
-    for (int i = len4 + threadIdx.x; i < len; i += SEL_THREADS) keys[i] = fkey(src[i]);
+    const uint32_t tq = __atomic_load_n(tau + q, __ATOMIC_RELAXED);
+    if (threadIdx.x == 0) nsurv = 0;
     __syncthreads();
+    int mine = 0;
+    auto keep = [&](float f) {
+        const uint32_t k = fkey(f);
+        const bool ok = k >= tq;
+        mine += ok;
+        return ok ? k : 0u;
+    };
+    // slab rows start 16-B aligned (S % 4 == 0, L % 4 == 0): float4 loads.
+    // A full chunk issues all of a thread's loads before the first LDS store
+    // (one memory latency per block instead of one per float4).
+    if (len == CHUNK_L) {
+        constexpr int PER = CHUNK_L / (SEL_THREADS * 4);
+        float4 v[PER];
+#pragma unroll
+        for (int j = 0; j < PER; ++j)
+            v[j] = reinterpret_cast<const float4*>(src)[threadIdx.x + j * SEL_THREADS];
+#pragma unroll
+        for (int j = 0; j < PER; ++j)
+            reinterpret_cast<uint4*>(keys)[threadIdx.x + j * SEL_THREADS] =
+                make_uint4(keep(v[j].x), keep(v[j].y), keep(v[j].z), keep(v[j].w));
+    } else {
+        const int len4 = len & ~3;
+        for (int i = threadIdx.x * 4; i < len4; i += SEL_THREADS * 4) {
+            const float4 v = *reinterpret_cast<const float4*>(src + i);
+            *reinterpret_cast<uint4*>(keys + i) = make_uint4(keep(v.x), keep(v.y), keep(v.z), keep(v.w));
+        }
+        for (int i = len4 + threadIdx.x; i < len; i += SEL_THREADS) keys[i] = keep(src[i]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&nsurv, mine);
+    __syncthreads();
+    const int nvalid = nsurv;
     const long long o = ((long long)q * nchunks + chunk0 + c) * KC;
     const int base = row0 + c * L;
-    block_topk([&](int i) { return keys[i]; }, [&](int i) { return base + i; }, len, KC, cand_k + o, cand_i + o, smi);
+    const uint32_t thr = block_topk<true>([&](int i) { return keys[i]; }, [&](int i) { return base + i; }, len, KC,
+                                          cand_k + o, cand_i + o, smi, nvalid);
+    if (threadIdx.x == 0 && nvalid > KC && thr > tq) atomicMax(tau + q, thr);
+}
+
+__global__ void k_zero_u32(uint32_t* p, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = 0u;
 }
 
 // ------------------------------------------------------------------ bitonic
@@ -320,7 +386,7 @@ static int pow2_at_least(int v) {
 struct KnnPlan {
     int L, nchunks, G, KC, npow2;
     long long S;
-    size_t slab_bytes, cand_bytes, sel_bytes, fin_bytes, total;
+    size_t slab_bytes, cand_bytes, sel_bytes, fin_bytes, tau_bytes, total;
 };
 
 static int default_cand(int k, int dtype) {
@@ -333,7 +399,7 @@ static KnnPlan plan(long long n_db, int nq, int k, int cand, int dtype) {
     p.KC = cand > 0 ? cand : default_cand(k, dtype);
     p.L = (int)(n_db < CHUNK_L ? n_db : CHUNK_L);
     p.nchunks = (int)((n_db + p.L - 1) / p.L);
-    long long g = (long long)(SLAB_BUDGET / ((size_t)nq * p.L * 4));
+    long long g = (long long)(slab_budget() / ((size_t)nq * p.L * 4));
     if (g < 1) g = 1;
     if (g > p.nchunks) g = p.nchunks;
     if (g * p.L > (4ll << 20)) g = (4ll << 20) / p.L;  // <= 4M rows per GEMM pass (grid.y limit)
@@ -345,7 +411,8 @@ static KnnPlan plan(long long n_db, int nq, int k, int cand, int dtype) {
     p.cand_bytes = (size_t)nq * p.nchunks * p.KC * 4;
     p.sel_bytes = ((size_t)nq * p.KC * 4 + 255) / 256 * 256;
     p.fin_bytes = ((size_t)nq * p.npow2 * 8 + 255) / 256 * 256 + ((size_t)nq * p.npow2 * 4 + 255) / 256 * 256;
-    p.total = p.slab_bytes + 2 * ((p.cand_bytes + 255) / 256 * 256) + 2 * p.sel_bytes + p.fin_bytes;
+    p.tau_bytes = ((size_t)nq * 4 + 255) / 256 * 256;
+    p.total = p.slab_bytes + 2 * ((p.cand_bytes + 255) / 256 * 256) + 2 * p.sel_bytes + p.fin_bytes + p.tau_bytes;
     return p;
 }
 
@@ -383,6 +450,7 @@ int rr_knn_topk(const void* db, const float* db_f32, long long n_db, const void*
     int* sel_i = (int*)(fws + p.sel_bytes);
     double* fin_s = (double*)(fws + 2 * p.sel_bytes);
     int* fin_i = (int*)(fws + 2 * p.sel_bytes + ((size_t)nq * p.npow2 * 8 + 255) / 256 * 256);
+    uint32_t* tau = (uint32_t*)(fws + 2 * p.sel_bytes + p.fin_bytes);
 
     static bool attr_done = false;
     if (!attr_done) {
@@ -393,6 +461,8 @@ int rr_knn_topk(const void* db, const float* db_f32, long long n_db, const void*
     }
 
     const size_t esz = dtype == RR_F32 ? 4 : 2;
+    // a kernel, not hipMemsetAsync: the reset must replay as an ordered node of a captured hipGraph
+    hipLaunchKernelGGL(k_zero_u32, dim3((nq + 255) / 256), dim3(256), 0, s, tau, nq);
     for (long long r0 = 0; r0 < n_db; r0 += (long long)p.G * p.L) {
         const int rows = (int)((n_db - r0) < (long long)p.G * p.L ? (n_db - r0) : (long long)p.G * p.L);
         ConvArgs a{};
@@ -407,7 +477,7 @@ int rr_knn_topk(const void* db, const float* db_f32, long long n_db, const void*
         gemm_scores(a, dtype, s);
         const int chunks = (rows + p.L - 1) / p.L;
         hipLaunchKernelGGL(k_chunk_select, dim3(nq, chunks), dim3(SEL_THREADS), (size_t)p.L * 4, s, slab, p.S, p.L,
-                           rows, (int)r0, (int)(r0 / p.L), p.nchunks, p.KC, cand_k, cand_i);
+                           rows, (int)r0, (int)(r0 / p.L), p.nchunks, p.KC, cand_k, cand_i, tau);
     }
     const size_t fin_lds = (size_t)p.npow2 * 12;
     if (fin_lds > 160 * 1024 - 4096) return fail(RR_EINVAL, "rr_knn_topk: candidate set exceeds LDS");

@@ -53,6 +53,31 @@ def test_knn_ties_lower_index_first(cuda):
     np.testing.assert_array_equal(i.cpu().numpy(), ref_i)
 
 
+def test_knn_running_screen_across_chunks(cuda):
+    """The chunk select drops keys below a query's running threshold (the best
+    K-th screening key of earlier chunks).  Databases that stress it, over
+    several 16384-row chunks: blocks duplicated across chunks (ties at the
+    threshold, lower index must win), rows whose scores rise chunk after chunk
+    (threshold overtaken every chunk), and all-equal rows (every key ties)."""
+    from cirtorch.search import KnnIndex
+    from oracle import data, ops
+    d = 256
+    base = data.unit_rows(20000, d, seed=41)
+    qq = data.unit_rows(5, d, seed=42)
+    dup = np.concatenate([base, base, base[:9000]], 0)                     # 49000 rows, 3 chunks+
+    # rising: row i = normalize(q0 * t_i + noise), t_i increasing with i
+    t = np.linspace(0.0, 1.0, 50000, dtype=np.float32)[:, None]
+    rise = qq[:1] * t + data.unit_rows(50000, d, seed=43)
+    rise = (rise / np.linalg.norm(rise, axis=1, keepdims=True)).astype(np.float32)
+    same = np.repeat(base[:1], 40000, 0)
+    for name, db in (("dup", dup), ("rise", rise), ("same", same)):
+        ref_s, ref_i = ops.topk_exact(db, qq, 100)
+        for prec in ("fp32", "bf16", "fp16"):
+            s, i = KnnIndex(torch.from_numpy(db).to(cuda), prec).search(torch.from_numpy(qq).to(cuda), 100)
+            np.testing.assert_array_equal(i.cpu().numpy(), ref_i, err_msg="%s %s" % (name, prec))
+            np.testing.assert_allclose(s.cpu().numpy(), ref_s, rtol=0, atol=1e-12)
+
+
 def test_knn_k_larger_than_db(cuda):
     from cirtorch.search import KnnIndex
     from oracle import data
