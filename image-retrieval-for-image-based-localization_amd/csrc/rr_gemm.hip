@@ -156,6 +156,10 @@ __global__ void __launch_bounds__(64 * WC * WP, ((NS == 2 && AK * TC <= 256) || 
     // same XCD instead of Infinity-Cache reads.  A bijection on [0, ntiles).
     // Within an XCD's range the order is pixel-tile-major, so the channel tiles
     // of one pixel tile run side by side and share its activations in L2.
+    // xmap bit 1: static priority for the second half of the waves (the
+    // arbitration loser of each SIMD pair), bit 0: XCD-contiguous tile order
+    if ((xmap & 2) && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+    xmap &= 1;
     const int n8 = xmap ? ntiles & ~7 : 0, per8 = n8 >> 3;
     const int tiles_c = ntiles / tiles_p;
     auto tile_at = [&](int lt) {  // -> channel-major tile index (c0 = t / tiles_p)
@@ -436,7 +440,9 @@ __global__ void __launch_bounds__(64 * WC * WP, ((NS == 2 && AK * TC <= 256) || 
     int ck = 0, ctile = 0;
     for (int s = 0; s < total; ++s) {
         const int cur = s % NS;
-        if (issued < total) { issue(issued++ % NS); xprefetch(); }
+        if constexpr (NS == 2) {
+            if (issued < total) { issue(issued++ % NS); xprefetch(); }
+        }
         // wait until this wave's step-s DMA is done (younger steps may stay in
         // flight; older epilogue VMEM ops are drained too), then barrier: everyone's.
         const int ahead = issued - s - 1;
@@ -444,6 +450,14 @@ __global__ void __launch_bounds__(64 * WC * WP, ((NS == 2 && AK * TC <= 256) || 
         else if (NS >= 3 && ahead == 2) wait_vm_barrier<(NS >= 3 ? 2 : 0) * NLD>();
         else if (ahead == 1) wait_vm_barrier<AK ? NIB : NLD>();  // AK: a step issues B only (A's one-time load is older)
         else wait_vm_barrier<0>();
+        // NS >= 3: ONE barrier per K-step.  The refill is issued after it, into
+        // stage (s + NS - 1) % NS == (s - 1) % NS, which every wave finished
+        // reading in step s - 1 (all of them have passed this barrier), so the
+        // end-of-step LDS barrier of the 2-stage ring is not needed; NS - 2
+        // steps stay in flight across the wait.
+        if constexpr (NS >= 3) {
+            if (issued < total) { issue(issued++ % NS); xprefetch(); }
+        }
         if constexpr (!XPREF) {
             if (ck == nk - 1) prefetch_res(B0{}, tile_at(ctile));
         }
@@ -486,7 +500,7 @@ __global__ void __launch_bounds__(64 * WC * WP, ((NS == 2 && AK * TC <= 256) || 
                         }
             }
         }
-        lds_barrier();  // every wave finished reading stage `cur` before it is refilled
+        if constexpr (NS == 2) lds_barrier();  // every wave finished reading stage `cur` before it is refilled
         if (++ck == nk) {
             const int t = tile_at(ctile);
             if constexpr (XPREF) {
@@ -509,6 +523,7 @@ static int g_stages = 0;
 static bool g_wide = true;
 static bool g_ast = false;
 static bool g_xmap = false;
+static bool g_prio = false;
 static bool g_env_done = false;
 
 static int num_cus() {
@@ -517,6 +532,8 @@ static int num_cus() {
         g_stages = (e && (e[0] == '3')) ? 3 : 2;
         const char* w = getenv("RR_GEMM_WIDE");
         g_wide = !(w && w[0] == '0');
+        const char* pr = getenv("RR_GEMM_PRIO");
+        g_prio = pr && pr[0] == '1';
         g_env_done = true;
     }
     return grid_cus();
@@ -536,13 +553,13 @@ static void launch_ns(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
     do {                                                                                                             \
         if (km == 1)                                                                                                 \
             hipLaunchKernelGGL((k_igemm<T, TO, TC, TP, WC, WP, 1, PV, NS, AK>), dim3(grid), dim3(64 * WC * WP), 0, s, \
-                               a, tiles_p, ntiles, g_xmap ? 1 : 0);                                                  \
+                               a, tiles_p, ntiles, (g_xmap ? 1 : 0) | (g_prio ? 2 : 0));                                                  \
         else if (km == 2)                                                                                            \
             hipLaunchKernelGGL((k_igemm<T, TO, TC, TP, WC, WP, 2, PV, NS, AK>), dim3(grid), dim3(64 * WC * WP), 0, s, \
-                               a, tiles_p, ntiles, g_xmap ? 1 : 0);                                                  \
+                               a, tiles_p, ntiles, (g_xmap ? 1 : 0) | (g_prio ? 2 : 0));                                                  \
         else                                                                                                         \
             hipLaunchKernelGGL((k_igemm<T, TO, TC, TP, WC, WP, 0, PV, NS, AK>), dim3(grid), dim3(64 * WC * WP), 0, s, \
-                               a, tiles_p, ntiles, g_xmap ? 1 : 0);                                                  \
+                               a, tiles_p, ntiles, (g_xmap ? 1 : 0) | (g_prio ? 2 : 0));                                                  \
     } while (0)
     if constexpr (std::is_same<T, TO>::value && (TC / WC / 16) % 2 == 0) {
         if (perm) {

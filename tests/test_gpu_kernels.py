@@ -60,6 +60,21 @@ def test_conv_tile_configs(cuda, cfg, case, prec):
         E.lib().rr_set_tuning(0, 0)
 
 
+@pytest.mark.parametrize("cfg", [1, 2, 5])
+@pytest.mark.parametrize("case", TILE_CASES)
+def test_conv_tile_configs_3stage(cuda, cfg, case):
+    """3-stage LDS ring (one barrier per K-step, refill issued after it) on the
+    4-wave tiles: exact on every conv shape."""
+    from cirtorch import _engine as E
+    E.check(E.lib().rr_set_tuning(0, cfg), "rr_set_tuning")
+    E.check(E.lib().rr_set_tuning(1, 3), "rr_set_tuning")
+    try:
+        _check_conv(cuda, case, "bf16", True)
+    finally:
+        E.lib().rr_set_tuning(0, 0)
+        E.lib().rr_set_tuning(1, 2)
+
+
 STREAM_CASES = [
     # HBM-bound bf16 1x1 shapes of the bottleneck blocks (rr_stream.hip), P >= 4096, ragged P
     (2, 64, 47, 51, 64, 1, 1, 0, False, True),

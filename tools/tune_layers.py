@@ -63,8 +63,9 @@ def main():
 
     # (label, {tuning key: value}); key 0 = tile config, 4 = XCD tile order
     # (label, {tuning key: value}); key 0 = tile config, 5 = streaming 1x1 kernel
-    variants = [("auto", {0: 0, 5: 1}), ("auto/noS", {0: 0, 5: 0})] + \
-               [(CFG[c], {0: c, 5: 0}) for c in CFG]
+    variants = [("auto", {0: 0, 5: 1, 1: 2}), ("auto/noS", {0: 0, 5: 0, 1: 2})] + \
+               [(CFG[c], {0: c, 5: 0, 1: 2}) for c in CFG] + \
+               [(CFG[c] + "s3", {0: c, 5: 0, 1: 3}) for c in (1, 2, 3, 5)]
     head = "%-14s %-26s" % ("layer", "P x Cout x K") + "".join("%12s" % v[0] for v in variants)
     print(head)
     for name, inp, st, res in calls:
@@ -81,6 +82,7 @@ def main():
                 row += "%12s" % "err"
         print(row, flush=True)
     E.lib().rr_set_tuning(0, 0)
+    E.lib().rr_set_tuning(1, 2)
     E.lib().rr_set_tuning(5, 1)
 
 
