@@ -7,6 +7,7 @@ packed conv weights [c_out, k_packed], descriptors row-major [n, D].
 
 import ctypes
 
+import numpy as np
 import torch
 
 from . import _engine as E
@@ -122,12 +123,30 @@ def pack_stem_weights(weight, dtype=torch.bfloat16):
     return out
 
 
+_UNIT_LUT = {}
+
+
+def pixels_to_unit(x):
+    """uint8 pixels -> float32 x / 255 with numpy's IEEE division (torchvision
+    ``to_tensor``): a 256-entry table computed on the host, gathered on the
+    device (torch's scalar division multiplies by the reciprocal, which differs
+    in the last bit for some pixel values)."""
+    lut = _UNIT_LUT.get(x.device)
+    if lut is None:
+        lut = torch.from_numpy(np.arange(256, dtype=np.float32) / np.float32(255.0)).to(x.device)
+        _UNIT_LUT[x.device] = lut
+    return lut[x.long()]
+
+
 def stem_conv_pool(img, wpk, scale, shift, leaky=True, slope=0.01, mean=None, std=None):
     """Fused normalise + conv1 7x7/s2/p3 + BN + act + maxpool 3x3/s2/p1
     (cirtorch/backbones/resnet.py:59-66): [N, 3, H, W] float32 -> [N, Hp, Wp, 64] in wpk's dtype
-    (bf16 or fp16)."""
+    (bf16 or fp16).  uint8 images are read as pixels (value / 255, torchvision
+    ``to_tensor``) by ``rr_stem_conv_pool_u8``: identical output to the float32
+    path on ``img.float() / 255``."""
     E.require_gpu(img, wpk, scale, shift)
-    img = img.contiguous().float()
+    u8 = img.dtype == torch.uint8
+    img = img.contiguous() if u8 else img.contiguous().float()
     n, c, h, w = img.shape
     if c != 3:
         raise RuntimeError("stem_conv_pool: expected 3-channel images, got %d" % c)
@@ -137,9 +156,10 @@ def stem_conv_pool(img, wpk, scale, shift, leaky=True, slope=0.01, mean=None, st
     do = mean is not None
     m = (ctypes.c_float * 3)(*mean) if do else (ctypes.c_float * 3)()
     s = (ctypes.c_float * 3)(*std) if do else (ctypes.c_float * 3)(1, 1, 1)
-    E.check(E.lib().rr_stem_conv_pool(E.ptr(img), n, h, w, m, s, int(do), E.ptr(wpk), E.ptr(scale), E.ptr(shift),
-                                      E.RR_ACT_LEAKY if leaky else E.RR_ACT_IDENTITY, float(slope), E.ptr(y), hp, wp,
-                                      E.dtype_code(wpk.dtype), _st()), "rr_stem_conv_pool")
+    fn = E.lib().rr_stem_conv_pool_u8 if u8 else E.lib().rr_stem_conv_pool
+    E.check(fn(E.ptr(img), n, h, w, m, s, int(do), E.ptr(wpk), E.ptr(scale), E.ptr(shift),
+               E.RR_ACT_LEAKY if leaky else E.RR_ACT_IDENTITY, float(slope), E.ptr(y), hp, wp,
+               E.dtype_code(wpk.dtype), _st()), "rr_stem_conv_pool")
     return y
 
 

@@ -207,11 +207,13 @@ class ResNet(nn.Module):
                                  residual=residual, leaky=st.leaky, slope=st.slope, perm32=st.perm)
 
     def forward(self, x, normalize=None):
-        """x: [N, 3, H, W] float32 on the GPU (already normalised unless
+        """x: [N, 3, H, W] float32 on the GPU, or uint8 pixels (read as x / 255) (already normalised unless
         ``normalize=(mean, std)`` is given, which fuses cirtorch/utils/image.py
         ``normalize`` into the first kernel).  Returns OrderedDict mod1..mod5."""
         plan = self._plan or self._build_plan()
         mean, std = normalize if normalize is not None else (None, None)
+        if x.dtype == torch.uint8 and plan["stem_fused"] is None:
+            x = _ops.pixels_to_unit(x)  # pixels -> [0, 1] (to_tensor); the fused stem reads uint8 itself
         if plan["stem_fused"] is not None:
             st = plan["stem"]
             t = _ops.stem_conv_pool(x, plan["stem_fused"], st.scale, st.shift, leaky=st.leaky, slope=st.slope,

@@ -91,6 +91,8 @@ class ImageRetrievalNet(nn.Module):
                 if do_prediction else None
             return OrderedDict([("ret_loss", None)]), OrderedDict([("ret_pred", ret_pred)])
         if isinstance(img, torch.Tensor):
+            if img.dtype == torch.uint8:  # pixels -> [0, 1] (to_tensor) for the resize / padding paths
+                img = _ops.pixels_to_unit(img)
             img = PackedSequence(list(img)) if img.dim() == 4 else PackedSequence([img])
         if len(scales) > 1:
             preds = []
@@ -165,6 +167,10 @@ def _load_pil(path, imsize, bbx=None):
     return img
 
 
+def _to_pixels(img):
+    return torch.from_numpy(np.asarray(img, dtype=np.uint8).transpose(2, 0, 1).copy())
+
+
 def _to_tensor(img):
     a = np.asarray(img, dtype=np.float32) / 255.0
     return torch.from_numpy(a.transpose(2, 0, 1).copy())
@@ -181,10 +187,16 @@ def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], 
     for i, item in enumerate(images):
         if isinstance(item, str):
             pil = _load_pil(item, image_size, bbxs[i] if bbxs is not None else None)
-            x = transform(pil) if transform is not None else _to_tensor(pil)
+            # no transform: the decoded uint8 pixels cross PCIe (1 B per channel) and
+            # the fused stem reads them as x / 255 (== _to_tensor, bit for bit)
+            x = transform(pil) if transform is not None else _to_pixels(pil)
         else:
             x = item
-        x = x.to(dev).float()
+        x = x.to(dev)
+        if x.dtype == torch.uint8 and (list(ms) != [1] or not normalize_in_net):
+            x = _ops.pixels_to_unit(x)
+        elif x.dtype != torch.uint8:
+            x = x.float()
         if not normalize_in_net and transform is None and net.meta.get("mean") is not None:
             m = torch.tensor(net.meta["mean"], device=dev)[:, None, None]
             s = torch.tensor(net.meta["std"], device=dev)[:, None, None]
@@ -194,7 +206,7 @@ def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], 
             net.augment = None
         try:
             if list(ms) == [1]:
-                v = net.extract([x])[:, 0]
+                v = net.extract(x[None] if x.dtype == torch.uint8 else [x])[:, 0]
             else:
                 acc = None
                 for s in ms:

@@ -30,7 +30,7 @@ namespace {
 typedef __attribute__((ext_vector_type(4))) float tf32x4_t;
 
 struct StemArgs {
-    const float* x;   // [n][3][h][w]
+    const void* x;    // [n][3][h][w] float32, or uint8 pixels (value / 255, torchvision ToTensor)
     const uint4* w;   // [64][256] bf16 (as 16-B chunks), PERM32 rows, k = kh*32 + kw*4 + ci
     const float* scale;
     const float* shift;
@@ -53,7 +53,7 @@ __device__ __forceinline__ unsigned bf16_key2(unsigned w) {
     return w ^ (neg * 0x7FFFu);
 }
 
-template <int PH, int PW, typename HT>
+template <int PH, int PW, typename HT, bool U8 = false>
 __global__ void __launch_bounds__(NT) k_stem_pool(StemArgs a, int tiles_w, int tiles_hw, int ntiles) {
     constexpr int SR = 2 * PH + 1, SC = 2 * PW + 1, NP = SR * SC, NF = (NP + 15) / 16;
     constexpr unsigned KNI = H16<HT>::NEG_INF ^ 0x7FFFu;  // order key of -inf (pool padding)
@@ -96,7 +96,7 @@ __global__ void __launch_bounds__(NT) k_stem_pool(StemArgs a, int tiles_w, int t
         int img, ph0, pw0;
         tile_origin(t, img, ph0, pw0);
         const int ir0 = 4 * ph0 - 5, ic0 = 4 * pw0 - 5;  // = 2 * (2 * p0 - 1) - 3
-        const float* src = a.x + (long long)img * 3 * plane;
+        const long long ibase = (long long)img * 3 * plane;
 #pragma unroll
         for (int u = 0; u < SPT; ++u) {
             const int slot = tid + NT * u;
@@ -105,7 +105,12 @@ __global__ void __launch_bounds__(NT) k_stem_pool(StemArgs a, int tiles_w, int t
             const bool ok = slot < NSLOT && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
             const long long o = ok ? (long long)ih * W + iw : 0;
 #pragma unroll
-            for (int ch = 0; ch < 3; ++ch) pf[u][ch] = ok ? src[ch * plane + o] : 0.f;
+            for (int ch = 0; ch < 3; ++ch) {
+                if constexpr (U8)  // IEEE division: the same float as torch's / numpy's x / 255
+                    pf[u][ch] = ok ? (float)((const unsigned char*)a.x)[ibase + ch * plane + o] / 255.f : 0.f;
+                else
+                    pf[u][ch] = ok ? ((const float*)a.x)[ibase + ch * plane + o] : 0.f;
+            }
         }
     };
     auto fill_store = [&](int t, int buf) {
@@ -256,9 +261,10 @@ extern "C" int rr_stem_pack_weights(const float* w, int c_out, int c_in, int kh,
     return check_launch("rr_stem_pack_weights");
 }
 
-extern "C" int rr_stem_conv_pool(const float* x, int n, int h, int w, const float* mean_host, const float* std_host,
-                                 int do_normalize, const void* wpk, const float* scale, const float* shift, int act,
-                                 float slope, void* y, int hp, int wp, int dtype, void* stream) {
+template <bool U8>
+static int stem_conv_pool(const void* x, int n, int h, int w, const float* mean_host, const float* std_host,
+                          int do_normalize, const void* wpk, const float* scale, const float* shift, int act,
+                          float slope, void* y, int hp, int wp, int dtype, void* stream) {
     if (dtype != RR_BF16 && dtype != RR_F16) return fail(RR_EINVAL, "rr_stem_conv_pool: bf16 / fp16 only");
     if (!x || !wpk || !scale || !shift || !y) return fail(RR_EINVAL, "rr_stem_conv_pool: null pointer");
     if (n <= 0 || h <= 0 || w <= 0) return fail(RR_EINVAL, "rr_stem_conv_pool: bad shape");
@@ -290,10 +296,25 @@ extern "C" int rr_stem_conv_pool(const float* x, int n, int h, int w, const floa
     const int g_stem_cus = grid_cus();
     const int grid = (int)(ntiles < g_stem_cus ? ntiles : g_stem_cus);
     if (dtype == RR_F16)
-        hipLaunchKernelGGL((k_stem_pool<PH, PW, f16_t>), dim3(grid), dim3(NT), 0, as_stream(stream), a, tiles_w,
+        hipLaunchKernelGGL((k_stem_pool<PH, PW, f16_t, U8>), dim3(grid), dim3(NT), 0, as_stream(stream), a, tiles_w,
                            tiles_w * tiles_h, (int)ntiles);
     else
-        hipLaunchKernelGGL((k_stem_pool<PH, PW, bf16_t>), dim3(grid), dim3(NT), 0, as_stream(stream), a, tiles_w,
-                       tiles_w * tiles_h, (int)ntiles);
+        hipLaunchKernelGGL((k_stem_pool<PH, PW, bf16_t, U8>), dim3(grid), dim3(NT), 0, as_stream(stream), a, tiles_w,
+                           tiles_w * tiles_h, (int)ntiles);
     return check_launch("rr_stem_conv_pool");
+}
+
+extern "C" int rr_stem_conv_pool(const float* x, int n, int h, int w, const float* mean_host, const float* std_host,
+                                 int do_normalize, const void* wpk, const float* scale, const float* shift, int act,
+                                 float slope, void* y, int hp, int wp, int dtype, void* stream) {
+    return stem_conv_pool<false>(x, n, h, w, mean_host, std_host, do_normalize, wpk, scale, shift, act, slope, y, hp,
+                                 wp, dtype, stream);
+}
+
+extern "C" int rr_stem_conv_pool_u8(const unsigned char* x, int n, int h, int w, const float* mean_host,
+                                    const float* std_host, int do_normalize, const void* wpk, const float* scale,
+                                    const float* shift, int act, float slope, void* y, int hp, int wp, int dtype,
+                                    void* stream) {
+    return stem_conv_pool<true>(x, n, h, w, mean_host, std_host, do_normalize, wpk, scale, shift, act, slope, y, hp,
+                                wp, dtype, stream);
 }

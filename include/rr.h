@@ -125,6 +125,14 @@ int rr_stem_pack_weights(const float* w, int c_out, int c_in, int kh, int kw, vo
 int rr_stem_conv_pool(const float* x, int n, int h, int w, const float* mean_host, const float* std_host,
                       int do_normalize, const void* wpk, const float* scale, const float* shift, int act,
                       float slope, void* y, int hp, int wp, int dtype, void* stream);
+/* Same, on uint8 pixels [n][3][h][w]: each value is x / 255 in float32 (the
+ * torchvision ToTensor the reference's loaders apply, datasets/generic/
+ * transform.py:128), so the result equals rr_stem_conv_pool on x / 255.
+ * A decoded image crosses PCIe as 1 B per channel instead of 4. */
+int rr_stem_conv_pool_u8(const unsigned char* x, int n, int h, int w, const float* mean_host,
+                         const float* std_host, int do_normalize, const void* wpk, const float* scale,
+                         const float* shift, int act, float slope, void* y, int hp, int wp, int dtype,
+                         void* stream);
 
 /* Bilinear resize, align_corners=False, NCHW float32 (one image).
  * Replaces nn.functional.interpolate(scale_factor=s, mode='bilinear',

@@ -130,3 +130,23 @@ def test_r50_batch128_chain_matches_small_chains(cuda):
     small = torch.cat([net.extract(x[i:i + 32]) for i in range(0, 128, 32)], dim=1)
     cos = cosines(big.cpu().numpy(), small.cpu().numpy())
     assert cos.min() > 1 - 1e-5, cos.min()
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp16", "fp32"])
+@pytest.mark.parametrize("hw", [(224, 224), (100, 130)])
+def test_uint8_images_equal_float_path(cuda, precision, hw):
+    """uint8 pixels (rr_stem_conv_pool_u8 reads x / 255 in the fused stem;
+    fp32 and the packed / multi-scale paths convert first) give descriptors
+    bit-identical to the float32 images x / 255 (torchvision to_tensor, the
+    reference loaders' datasets/generic/transform.py:128)."""
+    from cirtorch.models.GF_net import make_net
+    from cirtorch.models.init import random_init_
+    net = make_net("resnet18", precision=precision, mean=[0.485, 0.456, 0.406], std=[0.229, 0.224, 0.225])
+    random_init_(net, seed=3)
+    net = net.to(cuda).eval()
+    g = torch.Generator(device=cuda).manual_seed(7)
+    u8 = torch.randint(0, 256, (3, 3) + hw, generator=g, device=cuda, dtype=torch.uint8)
+    f = torch.from_numpy(u8.cpu().numpy().astype(np.float32) / np.float32(255.0)).to(cuda)
+    assert torch.equal(net.extract(u8), net.extract(f))
+    assert torch.equal(net.extract(list(u8)), net.extract(list(f)))
+    assert torch.equal(net.extract(u8, scales=(0.5, 1)), net.extract(f, scales=(0.5, 1)))

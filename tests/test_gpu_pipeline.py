@@ -91,3 +91,26 @@ def test_config4_rank_and_map(cuda):
     _, oranks = ops.rank_reference(ref_vecs.T.copy(), ref_q.T.copy())
     ref = ops.compute_map_revisited(oranks, gnd)
     assert abs(got["mAP"] - 100 * (ref["mapM"] + ref["mapH"]) / 2) < 1e-3 * 100
+
+
+def test_extract_vectors_uint8_files_equal_float_tensors(cuda, tmp_path):
+    """Image files go to the GPU as uint8 pixels (fused stem reads x / 255):
+    bit-identical to extract_vectors on the float32 to_tensor images (bf16 net,
+    fused stem) and to the fp32 net's float path."""
+    from PIL import Image
+    from cirtorch.models.GF_net import extract_vectors, make_net, _load_pil, _to_tensor
+    from cirtorch.models.init import random_init_
+    from oracle import data
+    paths = []
+    for i, im in enumerate(data.structured_images(2, 150, 200, seed=61)):
+        arr = (np.clip(im.transpose(1, 2, 0), 0, 1) * 255).astype(np.uint8)
+        p = os.path.join(str(tmp_path), "u%d.png" % i)
+        Image.fromarray(arr).save(p)
+        paths.append(p)
+    for prec in ("bf16", "fp32"):
+        net = make_net("resnet18", precision=prec, mean=MEAN, std=STD)
+        random_init_(net, seed=4)
+        net = net.to(cuda).eval()
+        a = extract_vectors(net, paths, 128)
+        b = extract_vectors(net, [_to_tensor(_load_pil(p, 128)) for p in paths], 128)
+        assert torch.equal(a, b), prec
