@@ -196,6 +196,7 @@ __global__ void __launch_bounds__(SEL_THREADS) k_chunk_select(const float* __res
     extern __shared__ __attribute__((aligned(16))) uint32_t keys[];  // L
     __shared__ int smi[TOPK_BINS + 64];
     __shared__ int nsurv;
+    __shared__ int wcnt[SEL_WAVES];
     const int q = blockIdx.x, c = blockIdx.y;
     const int len = min(L, rows_in_pass - c * L);
     const float* src = slab + (long long)q * S + (long long)c * L;
@@ -209,20 +210,76 @@ __global__ void __launch_bounds__(SEL_THREADS) k_chunk_select(const float* __res
         mine += ok;
         return ok ? k : 0u;
     };
+    const long long o = ((long long)q * nchunks + chunk0 + c) * KC;
+    const int base = row0 + c * L;
     // slab rows start 16-B aligned (S % 4 == 0, L % 4 == 0): float4 loads.
-    // A full chunk issues all of a thread's loads before the first LDS store
-    // (one memory latency per block instead of one per float4).
     if (len == CHUNK_L) {
+        // Full chunk: wave w owns the contiguous keys [1024 w, 1024 w + 1024),
+        // 4 float4 per lane, all loads issued before any use.  When at most KC
+        // keys survive the screen (every chunk after the first few of a
+        // search) they are emitted straight from registers in index order —
+        // wave prefix, then per float4 a lane scan — with no LDS staging and
+        // no radix pass; otherwise the keys go to LDS for block_topk.
         constexpr int PER = CHUNK_L / (SEL_THREADS * 4);
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
         float4 v[PER];
 #pragma unroll
-        for (int j = 0; j < PER; ++j)
-            v[j] = reinterpret_cast<const float4*>(src)[threadIdx.x + j * SEL_THREADS];
+        for (int j = 0; j < PER; ++j) v[j] = reinterpret_cast<const float4*>(src)[w * 256 + j * 64 + lane];
+        uint4 kq[PER];
+        int cnt[PER];
 #pragma unroll
-        for (int j = 0; j < PER; ++j)
-            reinterpret_cast<uint4*>(keys)[threadIdx.x + j * SEL_THREADS] =
-                make_uint4(keep(v[j].x), keep(v[j].y), keep(v[j].z), keep(v[j].w));
-    } else {
+        for (int j = 0; j < PER; ++j) {
+            const int m0 = mine;
+            kq[j] = make_uint4(keep(v[j].x), keep(v[j].y), keep(v[j].z), keep(v[j].w));
+            cnt[j] = mine - m0;
+        }
+#pragma unroll
+        for (int s2 = 32; s2 > 0; s2 >>= 1) mine += __shfl_xor(mine, s2, 64);
+        if (lane == 0) wcnt[w] = mine;
+        __syncthreads();
+        int nvalid = 0, before = 0;
+#pragma unroll
+        for (int j = 0; j < SEL_WAVES; ++j) {
+            nvalid += wcnt[j];
+            before += j < w ? wcnt[j] : 0;
+        }
+        if (nvalid <= KC) {
+            int run = before;
+#pragma unroll
+            for (int j = 0; j < PER; ++j) {
+                int x = cnt[j];
+#pragma unroll
+                for (int s2 = 1; s2 < 64; s2 <<= 1) {
+                    const int y = __shfl_up(x, s2, 64);
+                    if (lane >= s2) x += y;
+                }
+                int slot = run + x - cnt[j];
+                run += __shfl(x, 63, 64);
+                const uint32_t kk[4] = {kq[j].x, kq[j].y, kq[j].z, kq[j].w};
+                const int i0 = base + (w * 256 + j * 64 + lane) * 4;
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (kk[e] != 0u) {
+                        cand_k[o + slot] = kk[e];
+                        cand_i[o + slot] = i0 + e;
+                        ++slot;
+                    }
+            }
+            for (int i = nvalid + (int)threadIdx.x; i < KC; i += SEL_THREADS) {
+                cand_k[o + i] = 0u;
+                cand_i[o + i] = -1;
+            }
+            return;  // block-uniform branch
+        }
+#pragma unroll
+        for (int j = 0; j < PER; ++j) reinterpret_cast<uint4*>(keys)[w * 256 + j * 64 + lane] = kq[j];
+        __syncthreads();
+        const uint32_t thr = block_topk<true>([&](int i) { return keys[i]; }, [&](int i) { return base + i; }, len,
+                                              KC, cand_k + o, cand_i + o, smi, nvalid);
+        if (threadIdx.x == 0 && thr > tq) atomicMax(tau + q, thr);
+        return;
+    }
+    {
         const int len4 = len & ~3;
         for (int i = threadIdx.x * 4; i < len4; i += SEL_THREADS * 4) {
             const float4 v = *reinterpret_cast<const float4*>(src + i);
@@ -231,12 +288,10 @@ __global__ void __launch_bounds__(SEL_THREADS) k_chunk_select(const float* __res
         for (int i = len4 + threadIdx.x; i < len; i += SEL_THREADS) keys[i] = keep(src[i]);
     }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
+    for (int s2 = 32; s2 > 0; s2 >>= 1) mine += __shfl_xor(mine, s2, 64);
     if ((threadIdx.x & 63) == 0) atomicAdd(&nsurv, mine);
     __syncthreads();
     const int nvalid = nsurv;
-    const long long o = ((long long)q * nchunks + chunk0 + c) * KC;
-    const int base = row0 + c * L;
     const uint32_t thr = block_topk<true>([&](int i) { return keys[i]; }, [&](int i) { return base + i; }, len, KC,
                                           cand_k + o, cand_i + o, smi, nvalid);
     if (threadIdx.x == 0 && nvalid > KC && thr > tq) atomicMax(tau + q, thr);
