@@ -60,8 +60,9 @@ def parse():
     ap.add_argument("--pcie-steps", type=int, default=4, help="PCIe-inclusive extract sub-benchmark steps (0 = skip)")
     ap.add_argument("--local-kpts", type=int, default=2048, help="keypoints per image for the local-head sub-benchmark (0 = skip)")
     ap.add_argument("--latency", type=int, default=1, help="single-image extract latency, eager vs HIP-graph replay (0 = skip)")
-    ap.add_argument("--overlap", action="store_true",
-                    help="run batch i's match on a second stream, overlapping batch i+1's extract (measured slower on one GPU)")
+    ap.add_argument("--no-overlap", dest="overlap", action="store_false",
+                    help="run each step's match on the extraction stream (default: on a second stream, overlapping "
+                         "the next step's extraction; +0.8-1.5 %% on one GPU, DESIGN.md)")
     ap.add_argument("--cpu-images", type=int, default=2)
     ap.add_argument("--cpu-db-rows", type=int, default=100_000)
     return ap.parse_args()
@@ -423,9 +424,10 @@ def main():
         "dtype": args.precision,
         "data": "synthetic (U[0,1) images, random-init weights, counter-hash N(0,1) unit DB rows)",
         "config": {"workload": "%s-GeM+whiten %s extract %dx%d, B=%d/GPU (chains of %d), then top-%d cosine kNN of "
-                               "all %d queries vs %d x %d DB sharded over %d GPU(s)"
+                               "all %d queries vs %d x %d DB sharded over %d GPU(s)%s"
                                % (args.arch, args.precision, W, H, B, EB, args.k, B * world, args.db_rows, args.dim,
-                                  world),
+                                  world, "; each step's search on a second stream beside the next step's extraction"
+                                  if args.overlap else ""),
                    "global_batch": B * world, "extract_batch": EB, "image": [3, H, W], "db_rows": args.db_rows,
                    "dim": args.dim,
                    "k": args.k, "parallelism": "dp%d (images) x db-shard%d" % (world, world)},
