@@ -50,6 +50,7 @@ _SIGS = {
     "rr_maxpool2d": ([_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _i, _vp], _i),
     "rr_resize_bilinear": ([_vp, _i, _i, _i, _vp, _i, _i, _d, _d, _vp], _i),
     "rr_global_pool": ([_vp, _i, _i, _i, _i, _i, _f, _f, _vp, _i, _vp], _i),
+    "rr_global_pool_pdev": ([_vp, _i, _i, _i, _i, _i, _f, _vp, _f, _vp, _i, _vp], _i),
     "rr_l2n_rows": ([_vp, _i, _i, _f, _vp, _vp], _i),
     "rr_linear_rows": ([_vp, _i, _i, _vp, _vp, _i, _vp, _vp], _i),
     "rr_head_workspace_bytes": ([_i, _i], _sz),

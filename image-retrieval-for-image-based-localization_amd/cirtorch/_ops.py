@@ -164,14 +164,18 @@ def stem_conv_pool(img, wpk, scale, shift, leaky=True, slope=0.01, mean=None, st
 
 
 def resize_bilinear(img, scale_factor):
-    """img: [C, H, W] float32 -> bilinear (align_corners=False) resize by
-    scale_factor, output size floor(H*s) x floor(W*s) like
-    nn.functional.interpolate(scale_factor=s) (cirtorch/models/GF_net.py:32-35)."""
+    """img: [C, H, W] (or a same-size batch [N, C, H, W]) float32 -> bilinear
+    (align_corners=False) resize by scale_factor, output size floor(H*s) x
+    floor(W*s) like nn.functional.interpolate(scale_factor=s)
+    (cirtorch/models/GF_net.py:32-35).  Planes are independent, so a batch is
+    one launch over N*C planes."""
     E.require_gpu(img)
     img = img.contiguous().float()
-    c, h, w = img.shape
+    lead = img.shape[:-2]
+    h, w = img.shape[-2:]
+    c = int(np.prod(lead)) if len(lead) else 1
     ho, wo = int(h * scale_factor), int(w * scale_factor)
-    out = torch.empty((c, ho, wo), dtype=torch.float32, device=img.device)
+    out = torch.empty(tuple(lead) + (ho, wo), dtype=torch.float32, device=img.device)
     E.check(E.lib().rr_resize_bilinear(E.ptr(img), c, h, w, E.ptr(out), ho, wo, 1.0 / scale_factor,
                                        1.0 / scale_factor, _st()), "rr_resize_bilinear")
     return out
@@ -179,8 +183,19 @@ def resize_bilinear(img, scale_factor):
 
 # ---------------------------------------------------------------- head ops
 def global_pool(x, mode, p=3.0, eps=1e-6):
-    """x: [N, C, H, W] (NCHW-contiguous or channels_last view) -> [N, C] float32."""
+    """x: [N, C, H, W] (NCHW-contiguous or channels_last view) -> [N, C] float32.
+    p: a float, or a one-element GPU tensor (the learnable ``pool.p``) that the
+    kernel reads from device memory (rr_global_pool_pdev: no host read-back)."""
     E.require_gpu(x)
+    p_dev = None
+    if torch.is_tensor(p):
+        if p.numel() != 1:
+            raise NotImplementedError("per-channel GeM exponents (GeMmp) are out of scope")
+        E.require_gpu(p)
+        p_dev = p.detach().reshape(1)
+        if p_dev.dtype != torch.float32:
+            p_dev = p_dev.float()
+        p = 1.0
     n, c, h, w = x.shape
     if x.is_contiguous(memory_format=torch.channels_last) and not x.is_contiguous():
         layout = E.RR_NHWC
@@ -195,8 +210,12 @@ def global_pool(x, mode, p=3.0, eps=1e-6):
     if x.dtype not in (torch.float32, torch.bfloat16, torch.float16):
         x = x.float()
     out = torch.empty((n, c), dtype=torch.float32, device=x.device)
-    E.check(E.lib().rr_global_pool(E.ptr(x), n, c, h * w, layout, mode, float(p), float(eps), E.ptr(out),
-                                   E.dtype_code(x.dtype), _st()), "rr_global_pool")
+    if p_dev is not None:
+        E.check(E.lib().rr_global_pool_pdev(E.ptr(x), n, c, h * w, layout, mode, float(p), E.ptr(p_dev), float(eps),
+                                            E.ptr(out), E.dtype_code(x.dtype), _st()), "rr_global_pool_pdev")
+    else:
+        E.check(E.lib().rr_global_pool(E.ptr(x), n, c, h * w, layout, mode, float(p), float(eps), E.ptr(out),
+                                       E.dtype_code(x.dtype), _st()), "rr_global_pool")
     return out
 
 

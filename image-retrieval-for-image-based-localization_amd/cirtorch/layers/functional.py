@@ -12,24 +12,16 @@ from .. import _engine as E
 from .. import _ops
 
 
-_P_CACHE = {}
-
-
-def _p_value(p):
-    """Host value of the GeM exponent.  A GPU parameter is read back once per
-    version (``Tensor._version`` bumps on every in-place update, e.g.
-    ``load_state_dict``), so steady-state forwards issue no device->host sync
-    (which would drain the stream and break HIP-graph capture)."""
+def _p_arg(p):
+    """GeM exponent for the kernel: a learnable ``pool.p`` Parameter stays in
+    device memory and is read by the kernel itself (rr_global_pool_pdev), so
+    no forward reads it back to the host (no stream drain, graph-capturable)
+    and every update of it — load_state_dict, an optimizer step or an in-place
+    ``p.data.fill_`` — is seen by the next launch."""
     if torch.is_tensor(p):
         if p.numel() != 1:
             raise NotImplementedError("per-channel GeM exponents (GeMmp) are out of scope")
-        key = (p.data_ptr(), p.device, p._version)
-        v = _P_CACHE.get(key)
-        if v is None:
-            if len(_P_CACHE) > 64:
-                _P_CACHE.clear()
-            v = _P_CACHE[key] = float(p.detach().reshape(-1)[0].item())
-        return v
+        return p
     return float(p)
 
 
@@ -42,7 +34,7 @@ def spoc(x):
 
 
 def gem(x, p=3.0, eps=1e-6):
-    return _ops.global_pool(x, E.RR_POOL_GEM, _p_value(p), eps).unsqueeze(-1).unsqueeze(-1)
+    return _ops.global_pool(x, E.RR_POOL_GEM, _p_arg(p), eps).unsqueeze(-1).unsqueeze(-1)
 
 
 def l2n(x, eps=1e-6):

@@ -42,7 +42,7 @@ class globalHead(nn.Module):
         """[N, C, h, w] -> [N, C] float32 (one launch)."""
         from ... import _engine as E
         if isinstance(self.pool, GeM):
-            return _ops.global_pool(x, E.RR_POOL_GEM, LF._p_value(self.pool.p), self.pool.eps)
+            return _ops.global_pool(x, E.RR_POOL_GEM, LF._p_arg(self.pool.p), self.pool.eps)
         if isinstance(self.pool, MAC):
             return _ops.global_pool(x, E.RR_POOL_MAC)
         if isinstance(self.pool, SPoC):

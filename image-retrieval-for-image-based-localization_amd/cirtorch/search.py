@@ -35,28 +35,63 @@ def _rows(cols):
     return rows.float().contiguous()
 
 
+def _padded_dim(d, dtype):
+    """The engine's score GEMM takes power-of-two D >= 32 (>= 64 for fp16
+    screening); other D are zero-padded, which changes no dot product."""
+    p = 64 if dtype == torch.float16 else 32
+    while p < d:
+        p <<= 1
+    return p
+
+
+def _pad_cols(x, d_pad):
+    if x.shape[1] == d_pad:
+        return x
+    return torch.nn.functional.pad(x, (0, d_pad - x.shape[1])).contiguous()
+
+
 class KnnIndex:
     def __init__(self, db_rows, precision="fp32", cand=0, idx_offset=0):
-        """db_rows: [N, D] float32 on the GPU (kept by reference, not copied)."""
-        self.db32 = db_rows.float().contiguous()
+        """db_rows: [N, D] float32 on the GPU (kept by reference, not copied,
+        when D is a power of two >= 32; zero-padded otherwise)."""
         self.dtype = _PREC[precision]
-        self.db = _ops.cast_screen(self.db32, self.dtype)
+        self.dim = db_rows.shape[1]
+        self.d_pad = _padded_dim(self.dim, self.dtype)
+        self.db32 = _pad_cols(db_rows.float().contiguous(), self.d_pad)
+        self.db = _ops.cast_screen(self.db32, self.dtype) if self.db32.shape[0] else self.db32.to(self.dtype)
         self.cand = cand
         self.idx_offset = idx_offset
-        self._ws = None
+        self._ws = {}   # scratch per stream: searches on different streams never share a slab
 
     @property
     def ntotal(self):
         return self.db32.shape[0]
 
+    def _workspace(self, need, device):
+        """Scratch of the current stream.  A buffer is only ever used by the
+        stream it was allocated on, so concurrent searches of one index on two
+        streams do not race; a replaced buffer is freed in that stream's order."""
+        stream = torch.cuda.current_stream(device)
+        ws = self._ws.get(stream.cuda_stream)
+        if ws is None or ws.numel() < need:
+            ws = torch.empty(need, dtype=torch.uint8, device=device)
+            self._ws[stream.cuda_stream] = ws
+        return ws
+
     def search(self, q_rows, k):
-        q32 = q_rows.float().contiguous()
+        """q_rows [Q, D] -> (scores float64 [Q, k], idx int64 [Q, k]) on the current stream.
+        An empty shard (ntotal == 0) returns k (-inf, -1) entries per query, which
+        the sharded merge drops."""
+        if q_rows.shape[1] != self.dim:
+            raise RuntimeError("KnnIndex.search: queries have D=%d, the database D=%d" % (q_rows.shape[1], self.dim))
+        q32 = _pad_cols(q_rows.float().contiguous(), self.d_pad)
+        if self.ntotal == 0 or q32.shape[0] == 0:
+            s = torch.full((q32.shape[0], k), float("-inf"), dtype=torch.float64, device=q32.device)
+            return s, torch.full((q32.shape[0], k), -1, dtype=torch.int64, device=q32.device)
         q = _ops.cast_screen(q32, self.dtype)
         need = _ops.knn_workspace_bytes(self.ntotal, q.shape[0], q.shape[1], k, self.cand, self.dtype)
-        if self._ws is None or self._ws.numel() < need:
-            self._ws = torch.empty(need, dtype=torch.uint8, device=q.device)
         return _ops.knn_topk(self.db, self.db32, q, q32, k, cand=self.cand, idx_offset=self.idx_offset,
-                             workspace=self._ws)
+                             workspace=self._workspace(need, q.device))
 
 
 def knn(vecs, qvecs, k, precision="fp32", cand=0):

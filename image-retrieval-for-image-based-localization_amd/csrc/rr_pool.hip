@@ -18,12 +18,26 @@ __device__ __forceinline__ float powp(float x, float p, int ip) {
     return __powf(x, p);
 }
 
+// The exponent of a GeM parameter living in device memory (a learnable
+// ``pool.p``, pools.py:34) is read by the kernel itself: no host read-back, so
+// any update of the parameter (load_state_dict, optimizer step, in-place
+// ``p.data.fill_``) is seen by the next launch and a forward stays
+// graph-capturable.  pdev == nullptr: the host value p is used.
+__device__ __forceinline__ void gem_exponent(const float* pdev, float& p, int& ip) {
+    if (pdev) {
+        p = *pdev;
+        ip = (p == 3.f) ? 3 : (p == 2.f) ? 2 : (p == 1.f) ? 1 : 0;
+    }
+}
+
 // NHWC: [n][hw][c].  Block = 256 threads = 4 waves; each lane owns 4 channels
 // (one 16-B f32 / 8-B bf16 load per pixel), each wave a quarter of the pixels;
 // the 4 partial sums are combined through LDS.  grid = (ceil(c/256), n).
 template <typename T>
 __global__ void __launch_bounds__(256) k_pool_nhwc(const T* __restrict__ x, int c, int hw, int mode, float p,
-                                                   int ip, float eps, float* __restrict__ out) {
+                                                   int ip, const float* __restrict__ pdev, float eps,
+                                                   float* __restrict__ out) {
+    gem_exponent(pdev, p, ip);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int ch = blockIdx.x * 256 + lane * 4;
     const long long img = blockIdx.y;
@@ -79,7 +93,9 @@ __global__ void __launch_bounds__(256) k_pool_nhwc(const T* __restrict__ x, int 
 // combined through LDS in a fixed order.  grid = (ceil(c/512), n).
 template <typename H>
 __global__ void __launch_bounds__(1024) k_pool_nhwc_h16x8(const uint4* __restrict__ x, int c, int hw, int mode,
-                                                           float p, int ip, float eps, float* __restrict__ out) {
+                                                           float p, int ip, const float* __restrict__ pdev,
+                                                           float eps, float* __restrict__ out) {
+    gem_exponent(pdev, p, ip);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int c8 = c >> 3;
     const int g = blockIdx.x * 64 + lane;  // this lane's 8-channel group
@@ -136,7 +152,9 @@ __global__ void __launch_bounds__(1024) k_pool_nhwc_h16x8(const uint4* __restric
 // NCHW: one wave per (image, channel) plane of hw contiguous values.
 template <typename T>
 __global__ void __launch_bounds__(256) k_pool_nchw(const T* __restrict__ x, long long planes, int hw, int mode,
-                                                   float p, int ip, float eps, float* __restrict__ out) {
+                                                   float p, int ip, const float* __restrict__ pdev, float eps,
+                                                   float* __restrict__ out) {
+    gem_exponent(pdev, p, ip);
     const long long plane = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (plane >= planes) return;
@@ -240,9 +258,15 @@ extern "C" {
 
 int rr_global_pool(const void* x, int n, int c, int hw, int layout, int mode, float p, float eps, float* out,
                    int dtype, void* stream) {
+    if (mode == RR_POOL_GEM && !(p > 0.f)) return fail(RR_EINVAL, "rr_global_pool: GeM p must be > 0");
+    return rr_global_pool_pdev(x, n, c, hw, layout, mode, p, nullptr, eps, out, dtype, stream);
+}
+
+int rr_global_pool_pdev(const void* x, int n, int c, int hw, int layout, int mode, float p, const float* p_dev,
+                        float eps, float* out, int dtype, void* stream) {
     if (n <= 0 || c <= 0 || hw <= 0) return fail(RR_EINVAL, "rr_global_pool: empty input");
     if (mode < 0 || mode > 2) return fail(RR_EINVAL, "rr_global_pool: mode");
-    if (mode == RR_POOL_GEM && !(p > 0.f)) return fail(RR_EINVAL, "rr_global_pool: GeM p must be > 0");
+    const float* pdev = mode == RR_POOL_GEM ? p_dev : nullptr;
     int ip = (p == 3.f) ? 3 : (p == 2.f) ? 2 : (p == 1.f) ? 1 : 0;
     hipStream_t s = as_stream(stream);
     if (layout == RR_NHWC) {
@@ -250,27 +274,27 @@ int rr_global_pool(const void* x, int n, int c, int hw, int layout, int mode, fl
         dim3 grid((c + 255) / 256, n);
         if (dtype == RR_BF16 && c % 8 == 0 && ((uintptr_t)x & 15) == 0)
             hipLaunchKernelGGL(k_pool_nhwc_h16x8<bf16_t>, dim3((c + 511) / 512, n), dim3(1024), 0, s, (const uint4*)x, c, hw,
-                               mode, p, ip, eps, out);
+                               mode, p, ip, pdev, eps, out);
         else if (dtype == RR_F16 && c % 8 == 0 && ((uintptr_t)x & 15) == 0)
             hipLaunchKernelGGL(k_pool_nhwc_h16x8<f16_t>, dim3((c + 511) / 512, n), dim3(1024), 0, s, (const uint4*)x, c,
-                               hw, mode, p, ip, eps, out);
+                               hw, mode, p, ip, pdev, eps, out);
         else if (dtype == RR_BF16)
-            hipLaunchKernelGGL(k_pool_nhwc<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, c, hw, mode, p, ip, eps, out);
+            hipLaunchKernelGGL(k_pool_nhwc<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, c, hw, mode, p, ip, pdev, eps, out);
         else if (dtype == RR_F16)
-            hipLaunchKernelGGL(k_pool_nhwc<f16_t>, grid, dim3(256), 0, s, (const f16_t*)x, c, hw, mode, p, ip, eps, out);
+            hipLaunchKernelGGL(k_pool_nhwc<f16_t>, grid, dim3(256), 0, s, (const f16_t*)x, c, hw, mode, p, ip, pdev, eps, out);
         else if (dtype == RR_F32)
-            hipLaunchKernelGGL(k_pool_nhwc<float>, grid, dim3(256), 0, s, (const float*)x, c, hw, mode, p, ip, eps, out);
+            hipLaunchKernelGGL(k_pool_nhwc<float>, grid, dim3(256), 0, s, (const float*)x, c, hw, mode, p, ip, pdev, eps, out);
         else
             return fail(RR_EINVAL, "rr_global_pool: dtype");
     } else if (layout == RR_NCHW) {
         long long planes = (long long)n * c;
         dim3 grid((unsigned)((planes + 3) / 4));
         if (dtype == RR_BF16)
-            hipLaunchKernelGGL(k_pool_nchw<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, planes, hw, mode, p, ip, eps, out);
+            hipLaunchKernelGGL(k_pool_nchw<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, planes, hw, mode, p, ip, pdev, eps, out);
         else if (dtype == RR_F16)
-            hipLaunchKernelGGL(k_pool_nchw<f16_t>, grid, dim3(256), 0, s, (const f16_t*)x, planes, hw, mode, p, ip, eps, out);
+            hipLaunchKernelGGL(k_pool_nchw<f16_t>, grid, dim3(256), 0, s, (const f16_t*)x, planes, hw, mode, p, ip, pdev, eps, out);
         else if (dtype == RR_F32)
-            hipLaunchKernelGGL(k_pool_nchw<float>, grid, dim3(256), 0, s, (const float*)x, planes, hw, mode, p, ip, eps, out);
+            hipLaunchKernelGGL(k_pool_nchw<float>, grid, dim3(256), 0, s, (const float*)x, planes, hw, mode, p, ip, pdev, eps, out);
         else
             return fail(RR_EINVAL, "rr_global_pool: dtype");
     } else {

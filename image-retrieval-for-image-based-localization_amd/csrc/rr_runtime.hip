@@ -152,9 +152,9 @@ __global__ void k_maxpool_nhwc(const T* __restrict__ x, int n, int h, int w, int
 // for linear modes: src = scale*(dst+0.5)-0.5 clamped at 0.
 __global__ void k_resize_bilinear(const float* __restrict__ src, int c, int h, int w, float* __restrict__ dst,
                                   int ho, int wo, float sh, float sw) {
-    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    long long total = (long long)c * ho * wo;
-    if (i >= total) return;
+    const long long total = (long long)c * ho * wo;
+    const long long step = (long long)gridDim.x * blockDim.x;   // grid-stride: batches of any size
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += step) {
     int ox = (int)(i % wo);
     long long r = i / wo;
     int oy = (int)(r % ho);
@@ -170,6 +170,7 @@ __global__ void k_resize_bilinear(const float* __restrict__ src, int c, int h, i
     float v = ly0 * (lx0 * p[(long long)y0 * w + x0] + lx1 * p[(long long)y0 * w + x1]) +
               ly1 * (lx0 * p[(long long)y1 * w + x0] + lx1 * p[(long long)y1 * w + x1]);
     dst[i] = v;
+    }
 }
 
 // ------------------------------------------------------------ synthetic rows
@@ -215,26 +216,37 @@ __global__ void __launch_bounds__(256) k_fill_unit_rows(float* __restrict__ out,
     }
 }
 
+// Grid-stride casts: a dispatch holds < 2^32 work-items, so a 10M x 2048
+// database (2e10 elements, config 5) is covered by a capped grid looping.
 __global__ void k_cast_f32_f16(const float* __restrict__ x, f16_t* __restrict__ y, long long n) {
-    const long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
-    if (i + 3 < n) {
-        const float4 v = *reinterpret_cast<const float4*>(x + i);
-        y[i] = (f16_t)v.x; y[i + 1] = (f16_t)v.y; y[i + 2] = (f16_t)v.z; y[i + 3] = (f16_t)v.w;
-    } else {
-        for (long long j = i; j < n; ++j) y[j] = (f16_t)x[j];
+    const long long step = (long long)gridDim.x * blockDim.x * 4;
+    for (long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += step) {
+        if (i + 3 < n) {
+            const float4 v = *reinterpret_cast<const float4*>(x + i);
+            y[i] = (f16_t)v.x; y[i + 1] = (f16_t)v.y; y[i + 2] = (f16_t)v.z; y[i + 3] = (f16_t)v.w;
+        } else {
+            for (long long j = i; j < n; ++j) y[j] = (f16_t)x[j];
+        }
     }
 }
 
 __global__ void k_cast_f32_bf16(const float* __restrict__ x, bf16_t* __restrict__ y, long long n) {
-    long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
-    if (i + 3 < n) {
-        float4 v = *reinterpret_cast<const float4*>(x + i);
-        ushort4 o;
-        o.x = f2bf(v.x); o.y = f2bf(v.y); o.z = f2bf(v.z); o.w = f2bf(v.w);
-        *reinterpret_cast<ushort4*>(y + i) = o;
-    } else {
-        for (; i < n; ++i) y[i] = f2bf(x[i]);
+    const long long step = (long long)gridDim.x * blockDim.x * 4;
+    for (long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += step) {
+        if (i + 3 < n) {
+            float4 v = *reinterpret_cast<const float4*>(x + i);
+            ushort4 o;
+            o.x = f2bf(v.x); o.y = f2bf(v.y); o.z = f2bf(v.z); o.w = f2bf(v.w);
+            *reinterpret_cast<ushort4*>(y + i) = o;
+        } else {
+            for (long long j = i; j < n; ++j) y[j] = f2bf(x[j]);
+        }
     }
+}
+
+static inline unsigned cast_blocks(long long n) {
+    const long long b = (n + 1023) / 1024;       // 256 threads x 4 elements
+    return (unsigned)(b < (1ll << 20) ? (b > 0 ? b : 1) : (1ll << 20));
 }
 
 static inline unsigned nblk(long long total, int b) { return (unsigned)((total + b - 1) / b); }
@@ -311,14 +323,16 @@ int rr_resize_bilinear(const float* src, int c, int h, int w, float* dst, int ho
                        double scale_w, void* stream) {
     long long total = (long long)c * ho * wo;
     if (total <= 0) return fail(RR_EINVAL, "rr_resize_bilinear: empty");
-    hipLaunchKernelGGL(k_resize_bilinear, dim3(nblk(total, 256)), dim3(256), 0, as_stream(stream), src, c, h, w, dst,
+    const long long nb = (total + 255) / 256;
+    hipLaunchKernelGGL(k_resize_bilinear, dim3((unsigned)(nb < (1ll << 22) ? nb : (1ll << 22))), dim3(256), 0,
+                       as_stream(stream), src, c, h, w, dst,
                        ho, wo, (float)scale_h, (float)scale_w);
     return check_launch("rr_resize_bilinear");
 }
 
 int rr_fill_unit_rows(float* out, long long rows, int d, unsigned long long seed, long long row0, void* stream) {
     if (d <= 0 || d > 4096 || rows <= 0) return fail(RR_EINVAL, "rr_fill_unit_rows: d must be in (0, 4096]");
-    const long long maxgrid = 1ll << 30;
+    const long long maxgrid = 1ll << 23;  // 2^23 blocks x 256 threads: a dispatch holds < 2^32 work-items
     for (long long r = 0; r < rows; r += maxgrid) {
         long long cnt = rows - r < maxgrid ? rows - r : maxgrid;
         hipLaunchKernelGGL(k_fill_unit_rows, dim3((unsigned)cnt), dim3(256), 0, as_stream(stream), out + r * d, d,
@@ -330,14 +344,14 @@ int rr_fill_unit_rows(float* out, long long rows, int d, unsigned long long seed
 int rr_cast_f32_f16(const float* x, void* y, long long n, void* stream) {
     if (n <= 0) return RR_OK;
     if (!x || !y) return fail(RR_EINVAL, "rr_cast_f32_f16: null pointer");
-    hipLaunchKernelGGL(k_cast_f32_f16, dim3(nblk((n + 3) / 4, 256)), dim3(256), 0, as_stream(stream), x,
+    hipLaunchKernelGGL(k_cast_f32_f16, dim3(cast_blocks(n)), dim3(256), 0, as_stream(stream), x,
                        (f16_t*)y, n);
     return check_launch("rr_cast_f32_f16");
 }
 
 int rr_cast_f32_bf16(const float* x, void* y, long long n, void* stream) {
     if (n <= 0) return RR_OK;
-    hipLaunchKernelGGL(k_cast_f32_bf16, dim3(nblk((n + 3) / 4, 256)), dim3(256), 0, as_stream(stream), x,
+    hipLaunchKernelGGL(k_cast_f32_bf16, dim3(cast_blocks(n)), dim3(256), 0, as_stream(stream), x,
                        (bf16_t*)y, n);
     return check_launch("rr_cast_f32_bf16");
 }

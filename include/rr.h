@@ -147,6 +147,11 @@ int rr_resize_bilinear(const float* src, int c, int h, int w, float* dst, int ho
  * x layout RR_NHWC ([n][hw][c], any dtype) or RR_NCHW ([n][c][hw]). */
 int rr_global_pool(const void* x, int n, int c, int hw, int layout, int mode,
                    float p, float eps, float* out, int dtype, void* stream);
+/* Same, GeM exponent read by the kernel from DEVICE memory when p_dev != NULL
+ * (the learnable scalar `pool.p` Parameter, pools.py:34): no host read-back,
+ * so every update of the parameter is seen and the call stays graph-capturable. */
+int rr_global_pool_pdev(const void* x, int n, int c, int hw, int layout, int mode,
+                        float p, const float* p_dev, float eps, float* out, int dtype, void* stream);
 
 /* Row L2 normalisation y = x / (||x||_2 + eps) over `dim` contiguous floats.
  * Replaces cirtorch/modules/normalizations.py:9-16 (L2N). In-place allowed. */

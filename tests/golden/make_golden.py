@@ -189,7 +189,7 @@ def gen_ops():
 
 
 # ----------------------------------------------------------------------------- G1 / G2
-def gen_net(arch, res, n, seed, scales_list, fname, mixed=None):
+def gen_net(arch, res, n, seed, scales_list, fname, mixed=None, local=None):
     bias = centering_bias(arch)
     net, body = reference_net(arch, head_bias=bias)
     imgs = data.structured_images(n, res[0], res[1], seed=seed)
@@ -208,6 +208,22 @@ def gen_net(arch, res, n, seed, scales_list, fname, mixed=None):
         stages = _Body5(body)(x)
     for k in ("mod1", "mod2", "mod3", "mod4", "mod5"):
         out["chk_" + k] = stages[k][0].double().sum(dim=(1, 2)).numpy()
+    if local is not None:
+        # config 5: the reference localHead (local_head.py:19-71) on the stage map
+        # the local-feature config selects (local_config.ini:61 inputs = ["mod3"];
+        # its FPN is out of scope), keypoints / weights regenerated from the seed
+        from cirtorch.modules.heads.local_head import localHead as R_localHead
+        stage, npts, e, lseed = local
+        fm = stages[stage]
+        kp, lw, lb = data.local_head_problem(fm.shape[0], fm.shape[1], e, npts, lseed)
+        head = R_localHead(fm.shape[1], e)
+        head.load_state_dict({"whiten.weight": torch.from_numpy(lw), "whiten.bias": torch.from_numpy(lb)})
+        with torch.no_grad():
+            ref = head(fm, torch.from_numpy(kp)).numpy()
+        mine = ops.local_head(fm, torch.from_numpy(kp), torch.from_numpy(lw), torch.from_numpy(lb)).numpy()
+        assert np.abs(ref - mine).max() < 1e-5, np.abs(ref - mine).max()
+        out.update({"local_stage": np.array(stage), "local_npts": np.int64(npts), "local_e": np.int64(e),
+                    "local_seed": np.int64(lseed), "local_desc": ref})
     if mixed is not None:
         mimgs = [data.structured_images(1, h, w, seed=seed + 1 + i)[0] for i, (h, w) in enumerate(mixed)]
         ref = run_ref(net, mimgs)
@@ -244,27 +260,8 @@ def gen_knn():
 
 
 # ----------------------------------------------------------------------------- G5
-def synthetic_gnd(nq, ndb, seed):
-    r = data.rng(seed)
-    gnd = []
-    for _ in range(nq):
-        perm = r.permutation(ndb)
-        ne, nh, nj = r.integers(0, 40), r.integers(0, 30), r.integers(0, 10)
-        gnd.append({"easy": perm[:ne], "hard": perm[ne:ne + nh], "junk": perm[ne + nh:ne + nh + nj],
-                    "bbx": r.random(4)})
-    return gnd
-
-
 def gen_map():
-    nq, ndb = 70, 4993
-    db = data.unit_rows(ndb, 256, seed=501)
-    qq = data.unit_rows(nq, 256, seed=502)
-    gnd = synthetic_gnd(nq, ndb, seed=503)
-    # make the positives near-duplicates so the ranking is informative
-    r = data.rng(504)
-    for i, g in enumerate(gnd):
-        for j in np.concatenate([g["easy"], g["hard"]])[: r.integers(0, 20)]:
-            db[j] = db[j] + 0.3 * qq[i]
+    db, qq, gnd = data.map_problem()
     ranks = np.argsort(-np.dot(db, qq.T), axis=0)
     logs = []
     score = R_eval.compute_map_and_print("roxford5k", ranks, gnd, lambda *a: logs.append(a))
@@ -332,17 +329,103 @@ def gen_local():
     np.savez_compressed(os.path.join(HERE, "local.npz"), **out)
 
 
+# ----------------------------------------------------------------------------- G8
+def gen_nn_match():
+    """The reference mutual-NN matcher itself (HPatchesEval.py:23-43).  That
+    module imports cv2 at the top (for RANSAC homographies, not used by
+    get_desc_dist / nn_matcher); cv2 is absent, so a test-only empty ``cv2``
+    module is registered while it is imported (same recipe as inplace_abn)."""
+    had = "cv2" in sys.modules
+    if not had:
+        sys.modules["cv2"] = types.ModuleType("cv2")
+    try:
+        from cirtorch.utils.evaluation import HPatchesEval as R_hp
+    finally:
+        if not had:
+            del sys.modules["cv2"]
+    out = {}
+    for tag, (n1, n2, d, seed) in (("a", (300, 260, 128, 801)), ("b", (2048, 1900, 128, 802)), ("c", (7, 9, 16, 803))):
+        d1, d2 = data.nn_descriptors(n1, n2, d, seed)
+        dist = R_hp.get_desc_dist({"descriptors": d1}, {"descriptors": d2})
+        match = R_hp.nn_matcher(dist)
+        assert (match == ops.nn_matcher(d1, d2)).all()
+        out["shape_" + tag] = np.array([n1, n2, d, seed])
+        out["match_" + tag] = match.astype(np.int64)
+        print("  nn %s: %d mutual of %d" % (tag, (match >= 0).sum(), n1))
+    np.savez_compressed(os.path.join(HERE, "nnmatch.npz"), **out)
+
+
+# ----------------------------------------------------------------------------- G9
+def gen_transform():
+    """ISSTestTransform (cirtorch/datasets/generic/transform.py:81-130) run
+    unmodified on synthetic PIL images.  The module imports torchvision only for
+    ``functional.to_tensor`` (absent here): a test-only stand-in with the
+    published to_tensor of an RGB PIL image (HWC uint8 -> CHW float32 / 255) is
+    registered while it is loaded.  The file is loaded directly so the dataset
+    package __init__ (PIL-less dataset.py, samplers) is not imported."""
+    import importlib.util
+    from PIL import Image
+    tv = types.ModuleType("torchvision")
+    tvt = types.ModuleType("torchvision.transforms")
+    tvf = types.ModuleType("torchvision.transforms.functional")
+
+    def to_tensor(pic):
+        a = np.asarray(pic, dtype=np.uint8)
+        return torch.from_numpy(a.transpose(2, 0, 1).copy()).float().div(255)
+
+    tvf.to_tensor = to_tensor
+    tvt.functional = tvf
+    tv.transforms = tvt
+    saved = {k: sys.modules.get(k) for k in ("torchvision", "torchvision.transforms", "torchvision.transforms.functional")}
+    sys.modules.update({"torchvision": tv, "torchvision.transforms": tvt, "torchvision.transforms.functional": tvf})
+    try:
+        spec = importlib.util.spec_from_file_location(
+            "ref_generic_transform", os.path.join(REF, "cirtorch", "datasets", "generic", "transform.py"))
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                sys.modules.pop(k, None)
+            else:
+                sys.modules[k] = v
+    out = {}
+    cfgs = [(64, 96, [0.8, 1.2]), (80, 80, [0.8, 1.2]), (48, 200, [0.8, 1.2])]
+    for ci, (short, longest, rs) in enumerate(cfgs):
+        tf = mod.ISSTestTransform(shortest_size=short, longest_max_size=longest, random_scale=rs)
+        for ii, (w, h, bbx, pix) in enumerate(data.transform_images()):
+            img = Image.fromarray(pix, mode="RGB")
+            t = tf(img, bbx=bbx)["img"]
+            u8 = np.rint(t.numpy() * 255.0).astype(np.uint8)
+            assert np.array_equal(u8.astype(np.float32) / np.float32(255.0), t.numpy())
+            out["out_%d_%d" % (ci, ii)] = u8
+        out["cfg_%d" % ci] = np.array([short, longest])
+    np.savez_compressed(os.path.join(HERE, "transform.npz"), **out)
+
+
+GENERATORS = {
+    "ops": lambda: gen_ops(),
+    "r18": lambda: gen_net("resnet18", (224, 224), 8, 1001, [(1,), (0.5, 1, 2)], "r18.npz",
+                           mixed=[(200, 240), (224, 192), (160, 160)]),
+    "r50": lambda: gen_net("resnet50", (768, 1024), 2, 2001, [(1,)], "r50.npz"),
+    "r50ms": lambda: gen_net("resnet50", (384, 512), 1, 2101, [(0.5, 1, 2)], "r50ms.npz"),
+    "r101": lambda: gen_net("resnet101", (256, 320), 2, 2201, [(1,)], "r101.npz"),
+    # config 3: R101 multi-scale x0.5/1/2 at the 768x1024 workload size
+    "r101ms": lambda: gen_net("resnet101", (768, 1024), 1, 2301, [(1,), (0.5, 1, 2)], "r101ms.npz"),
+    # config 5: R152 at 768x1024 + the local head on mod3
+    "r152": lambda: gen_net("resnet152", (768, 1024), 1, 2401, [(1,)], "r152.npz", local=("mod3", 512, 128, 2402)),
+    "knn": lambda: gen_knn(),
+    "map": lambda: gen_map(),
+    "whiten": lambda: gen_whiten(),
+    "local": lambda: gen_local(),
+    "nnmatch": lambda: gen_nn_match(),
+    "transform": lambda: gen_transform(),
+}
+
+
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] == "local":
-        print("G7 local head"); gen_local(); sys.exit(0)
-    print("G3 ops"); gen_ops()
-    print("G1 resnet18@224"); gen_net("resnet18", (224, 224), 8, 1001, [(1,), (0.5, 1, 2)], "r18.npz",
-                                      mixed=[(200, 240), (224, 192), (160, 160)])
-    print("G2 resnet50@768x1024"); gen_net("resnet50", (768, 1024), 2, 2001, [(1,)], "r50.npz")
-    print("G2b resnet50 ms@384x512"); gen_net("resnet50", (384, 512), 1, 2101, [(0.5, 1, 2)], "r50ms.npz")
-    print("G2c resnet101@256x320"); gen_net("resnet101", (256, 320), 2, 2201, [(1,)], "r101.npz")
-    print("G4 knn"); gen_knn()
-    print("G5 map"); gen_map()
-    print("G6 whiten"); gen_whiten()
-    print("G7 local head"); gen_local()
+    names = sys.argv[1:] or list(GENERATORS)
+    for name in names:
+        print("golden", name)
+        GENERATORS[name]()
     print("done")
