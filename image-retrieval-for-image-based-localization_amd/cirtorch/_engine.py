@@ -54,6 +54,8 @@ _SIGS = {
     "rr_l2n_rows": ([_vp, _i, _i, _f, _vp, _vp], _i),
     "rr_linear_rows": ([_vp, _i, _i, _vp, _vp, _i, _vp, _vp], _i),
     "rr_head_workspace_bytes": ([_i, _i], _sz),
+    "rr_whiten_workspace_bytes": ([_i, _i], _sz),
+    "rr_whitenapply": ([_vp, _i, _i, _vp, _vp, _i, _vp, _vp, _sz, _vp], _i),
     "rr_head_l2n_whiten_l2n": ([_vp, _i, _i, _vp, _vp, _i, _f, _vp, _vp, _vp], _i),
     "rr_knn_workspace_bytes": ([_ll, _i, _i, _i, _i, _i], _sz),
     "rr_knn_topk": ([_vp, _vp, _ll, _vp, _vp, _i, _i, _i, _i, _ll, _vp, _vp, _vp, _sz, _i, _vp], _i),

@@ -257,6 +257,22 @@ def head_tail(pooled, weight, bias, whiten=True, eps=1e-6):
     return y
 
 
+def whitenapply_rows(x, m, P, d_out):
+    """x [N, D] float32 rows, m [D] / P [>= d_out, D] float64 (GPU) ->
+    L2N(P[:d_out] (x - m)) [N, d_out] float32, computed in float64 on the f64
+    MFMA (cirtorch/utils/whiten.py:4-12)."""
+    E.require_gpu(x, m, P)
+    x = x.contiguous().float()
+    m = m.contiguous().double().reshape(-1)
+    P = P.contiguous().double()
+    rows, dim = x.shape
+    y = torch.empty((rows, d_out), dtype=torch.float32, device=x.device)
+    ws = torch.empty(max(1, int(E.lib().rr_whiten_workspace_bytes(rows, d_out))), dtype=torch.uint8, device=x.device)
+    E.check(E.lib().rr_whitenapply(E.ptr(x), rows, dim, E.ptr(m), E.ptr(P), int(d_out), E.ptr(y), E.ptr(ws),
+                                   ws.numel(), _st()), "rr_whitenapply")
+    return y
+
+
 # ---------------------------------------------------------------- matching
 def knn_workspace_bytes(n_db, nq, d, k, cand=0, dtype=torch.float32):
     return int(E.lib().rr_knn_workspace_bytes(int(n_db), int(nq), int(d), int(k), int(cand), E.dtype_code(dtype)))

@@ -14,22 +14,24 @@ from .. import _ops
 
 
 def whitenapply(X, m, P, dimensions=None):
-    """X: D x N (numpy or torch).  Returns the same kind it was given."""
+    """X: D x N (numpy or torch) -> P[:dimensions] (X - m), columns L2-normalised
+    (+1e-6 on the norm, ``whiten.py:10``).  The arithmetic is float64, as in
+    the reference (numpy promotes the float32 vectors to the float64 m, P of
+    whitenlearn), on the GPU's f64 MFMA (``rr_whitenapply``); the result is
+    float32 columns (numpy input -> numpy output)."""
     was_numpy = not torch.is_tensor(X)
     if not dimensions:
         dimensions = P.shape[0]
     Xt = torch.as_tensor(np.asarray(X) if was_numpy else X)
-    out_dtype = Xt.dtype
-    Xt = Xt.cuda().float()
-    mt = torch.as_tensor(np.asarray(m) if not torch.is_tensor(m) else m).cuda().float().reshape(-1)
-    Pt = torch.as_tensor(np.asarray(P) if not torch.is_tensor(P) else P).cuda().float()[:dimensions].contiguous()
-    rows = (Xt.t() - mt[None, :]).contiguous()           # [N, D] centred rows
-    y = _ops.linear_rows(rows, Pt, None)                  # [N, d]
-    y = _ops.l2n_rows(y, 1e-6)
+    dev = Xt.device if Xt.is_cuda else torch.device("cuda")
+    rows = Xt.t().to(dev).float().contiguous()                                    # [N, D]
+    mt = torch.as_tensor(np.asarray(m) if not torch.is_tensor(m) else m).to(dev).double().reshape(-1)
+    Pt = torch.as_tensor(np.asarray(P) if not torch.is_tensor(P) else P).to(dev).double()
+    y = _ops.whitenapply_rows(rows, mt, Pt, int(dimensions))                       # [N, d]
     Y = y.t()
     if was_numpy:
-        return Y.cpu().numpy().astype(np.asarray(X).dtype, copy=False)
-    return Y.to(out_dtype)
+        return Y.cpu().numpy()
+    return Y
 
 
 def pcawhitenlearn(X):

@@ -250,6 +250,93 @@ __global__ void __launch_bounds__(512) k_linear_mfma(const float* __restrict__ x
     }
 }
 
+
+// Post-hoc learned whitening (cirtorch/utils/whiten.py:4-12, applied by
+// scripts/test.py:253-254) in the reference's arithmetic type: numpy promotes
+// the float32 descriptors to float64 against the float64 (m, P) of
+// whitenlearn, so y = P[:d] (x - m) and the L2 norm run in float64 here too,
+// on the f64 MFMA (v_mfma_f64_16x16x4_f64).  Whitening matrices amplify
+// directions of small variance, so a float32 GEMM loses ~1e-3 absolute on
+// the output; float64 keeps it at the final float32 rounding.
+// Block = 8 waves, 16 outputs x 64 rows; wave w takes the K-slices kb = w,
+// w + 8, ... of 16 inputs; lane (r = lane & 15, g = lane >> 4) loads
+// P[o0 + r][16 kb + 4 g .. + 3] and x[row + r][...] (centred in f64), MFMA e
+// of the four uses component e.  f64 C/D layout: col = lane & 15,
+// row = (lane >> 4) + 4 e.  Partial tiles reduced through LDS in fixed order.
+typedef __attribute__((ext_vector_type(4))) double lf64x4_t;
+__global__ void __launch_bounds__(512) k_whiten_f64(const float* __restrict__ x, int rows, int dim,
+                                                    const double* __restrict__ m, const double* __restrict__ P,
+                                                    int d_out, double* __restrict__ y) {
+    constexpr int RG = 4;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = lane & 15, g = lane >> 4;
+    const int o0 = blockIdx.x * 16, row0 = blockIdx.y * 16 * RG;
+    __shared__ double part[8][RG][64][4];
+    lf64x4_t acc[RG];
+#pragma unroll
+    for (int j = 0; j < RG; ++j) acc[j] = (lf64x4_t){0.0, 0.0, 0.0, 0.0};
+    const int nkb = dim / 16;
+    const bool orow = o0 + r < d_out;
+    const double* pr = P + (long long)(orow ? o0 + r : 0) * dim;
+    for (int kb = wave; kb < nkb; kb += 8) {
+        const int k = kb * 16 + g * 4;
+        double a[4];
+        if (orow) {
+            const double2 a01 = *reinterpret_cast<const double2*>(pr + k);
+            const double2 a23 = *reinterpret_cast<const double2*>(pr + k + 2);
+            a[0] = a01.x; a[1] = a01.y; a[2] = a23.x; a[3] = a23.y;
+        } else {
+            a[0] = a[1] = a[2] = a[3] = 0.0;
+        }
+        const double2 m01 = *reinterpret_cast<const double2*>(m + k);
+        const double2 m23 = *reinterpret_cast<const double2*>(m + k + 2);
+        double b[RG][4];
+#pragma unroll
+        for (int j = 0; j < RG; ++j) {
+            const int row = row0 + j * 16 + r;
+            if (row < rows) {
+                const float4 v = *reinterpret_cast<const float4*>(x + (long long)row * dim + k);
+                b[j][0] = (double)v.x - m01.x; b[j][1] = (double)v.y - m01.y;
+                b[j][2] = (double)v.z - m23.x; b[j][3] = (double)v.w - m23.y;
+            } else {
+                b[j][0] = b[j][1] = b[j][2] = b[j][3] = 0.0;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < RG; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[e], b[j][e], acc[j], 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < RG; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) part[wave][j][lane][e] = acc[j][e];
+    __syncthreads();
+    for (int t = threadIdx.x; t < RG * 64 * 4; t += 512) {
+        const int j = t >> 8, L = (t >> 2) & 63, e = t & 3;
+        double v = part[0][j][L][e];
+#pragma unroll
+        for (int q = 1; q < 8; ++q) v += part[q][j][L][e];
+        const int o = o0 + (L >> 4) + 4 * e, row = row0 + j * 16 + (L & 15);
+        if (o < d_out && row < rows) y[(long long)row * d_out + o] = v;
+    }
+}
+
+// y32 = y / (||y||_2 + eps) per row, norm in float64 (whiten.py:10), fixed order.
+__global__ void __launch_bounds__(256) k_l2n_rows_f64(const double* __restrict__ y, int dim, double eps,
+                                                      float* __restrict__ out) {
+    const long long row = blockIdx.x;
+    const double* yr = y + row * dim;
+    __shared__ double red[4];
+    double ss = 0.0;
+    for (int i = threadIdx.x; i < dim; i += 256) ss = fma(yr[i], yr[i], ss);
+    ss = wave_sum_d(ss);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+    __syncthreads();
+    const double nrm = sqrt((red[0] + red[1]) + (red[2] + red[3])) + eps;
+    for (int i = threadIdx.x; i < dim; i += 256) out[row * dim + i] = (float)(yr[i] / nrm);
+}
+
 }  // namespace rr
 
 using namespace rr;
@@ -332,6 +419,28 @@ int rr_head_l2n_whiten_l2n(const float* x, int rows, int dim, const float* w, co
     rc = rr_linear_rows(t0, rows, dim, w, b, dim, t1, stream);
     if (rc) return rc;
     return rr_l2n_rows(t1, rows, dim, eps, y, stream);
+}
+
+size_t rr_whiten_workspace_bytes(int rows, int d_out) { return (size_t)rows * d_out * sizeof(double); }
+
+int rr_whitenapply(const float* x, int rows, int dim, const double* m, const double* P, int d_out, float* y,
+                   void* workspace, size_t workspace_bytes, void* stream) {
+    if (rows <= 0 || dim <= 0 || d_out <= 0) return fail(RR_EINVAL, "rr_whitenapply: empty");
+    if (dim % 16) return fail(RR_EINVAL, "rr_whitenapply: dim must be a multiple of 16");
+    if (d_out > dim) return fail(RR_EINVAL, "rr_whitenapply: d_out > dim");
+    if ((((uintptr_t)x) | ((uintptr_t)m) | ((uintptr_t)P)) & 15)
+        return fail(RR_EINVAL, "rr_whitenapply: x, m and P must be 16-byte aligned");
+    if (!workspace || workspace_bytes < rr_whiten_workspace_bytes(rows, d_out))
+        return fail(RR_ENOSPACE, "rr_whitenapply: workspace too small");
+    hipStream_t s = as_stream(stream);
+    double* t = (double*)workspace;
+    for (int r0 = 0; r0 < rows; r0 += 1 << 20) {  // <= 16384 row blocks per launch
+        const int n = rows - r0 < (1 << 20) ? rows - r0 : (1 << 20);
+        hipLaunchKernelGGL(k_whiten_f64, dim3((d_out + 15) / 16, (n + 63) / 64), dim3(512), 0, s,
+                           x + (long long)r0 * dim, n, dim, m, P, d_out, t + (long long)r0 * d_out);
+    }
+    hipLaunchKernelGGL(k_l2n_rows_f64, dim3(rows), dim3(256), 0, s, t, d_out, 1e-6, y);
+    return check_launch("rr_whitenapply");
 }
 
 }  // extern "C"

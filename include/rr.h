@@ -170,6 +170,17 @@ size_t rr_head_workspace_bytes(int rows, int dim);
 int rr_head_l2n_whiten_l2n(const float* x, int rows, int dim, const float* w, const float* b,
                            int whiten, float eps, float* y, void* workspace, void* stream);
 
+/* Post-hoc learned whitening, y = L2N(P[:d_out] (x - m)) per row, computed in
+ * float64 on the f64 MFMA like the reference (cirtorch/utils/whiten.py:4-12:
+ * numpy promotes the float32 vectors to the float64 m, P of whitenlearn;
+ * applied at scripts/test.py:253-254).  x [rows][dim] float32 (dim % 16 == 0),
+ * m [dim] float64, P [>= d_out][dim] float64 row-major, y [rows][d_out]
+ * float32 (the float64 result rounded once).  L2N adds 1e-6 to the norm.
+ * workspace: rr_whiten_workspace_bytes(rows, d_out). */
+size_t rr_whiten_workspace_bytes(int rows, int d_out);
+int rr_whitenapply(const float* x, int rows, int dim, const double* m, const double* P, int d_out,
+                   float* y, void* workspace, size_t workspace_bytes, void* stream);
+
 /* --------------------------------------------------------------- matching */
 
 /* Brute-force cosine kNN with exact ordering.

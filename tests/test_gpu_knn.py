@@ -120,15 +120,27 @@ def test_topk_merge_equals_single_shard(cuda):
 
 def test_fp16_screening_copy_and_limits(cuda):
     """The fp16 screening copy is IEEE binary16 round-to-nearest-even (== torch
-    .half()); fp16 screening needs d >= 64."""
+    .half()); the engine's fp16 score GEMM needs d >= 64 (the C ABI refuses
+    less), KnnIndex zero-pads other widths (D = 32, 16, 100, 300) and returns
+    the exact results."""
+    from cirtorch import _engine as E
     from cirtorch import _ops
     from cirtorch.search import KnnIndex
-    from oracle import data
+    from oracle import data, ops
     x = torch.randn(1003, 64, device=cuda) * 3.0
     assert torch.equal(_ops.cast_f16(x), x.half())
     db = torch.from_numpy(data.unit_rows(100, 32, seed=5)).to(cuda)
     with pytest.raises(RuntimeError, match="d >= 64"):
-        KnnIndex(db, "fp16").search(db[:2], 3)
+        _ops.knn_topk(db.half(), db, db[:2].half(), db[:2], 3)
+    assert E.lib().rr_last_error()
+    for d in (32, 16, 100, 300):
+        dbn = data.unit_rows(700, d, seed=d)
+        qn = data.unit_rows(3, d, seed=d + 1)
+        ref_s, ref_i = ops.topk_exact(dbn, qn, 9)
+        for prec in ("fp16", "bf16", "fp32"):
+            s, i = KnnIndex(torch.from_numpy(dbn).to(cuda), prec).search(torch.from_numpy(qn).to(cuda), 9)
+            np.testing.assert_array_equal(i.cpu().numpy(), ref_i, err_msg="%d %s" % (d, prec))
+            np.testing.assert_allclose(s.cpu().numpy(), ref_s, rtol=0, atol=1e-12)
 
 
 def test_knn_full_size_1m_bench_shape(cuda):

@@ -119,3 +119,19 @@ def test_empty_shard_search_contributes_sentinels():
     idx = KnnIndex(torch.empty((0, 64)), "bf16", idx_offset=3)
     s, i = idx.search(torch.rand(5, 64), 7)
     assert s.shape == (5, 7) and torch.isinf(s).all() and (s < 0).all() and (i == -1).all()
+
+
+def test_synthetic_generators_match_fixture_recipes():
+    """cirtorch.utils.synthetic (used by bench.py's parity fields) draws exactly
+    the parameters / images the fixtures were generated from."""
+    from cirtorch.utils import synthetic
+    from oracle import data, weights
+    for arch in ("resnet18", "resnet50", "resnet152"):
+        a, b = synthetic.backbone_state(arch), weights.backbone_state(arch)
+        assert list(a) == list(b)
+        for k in a:
+            assert np.array_equal(a[k], b[k]), (arch, k)
+    for dim in (512, 2048):
+        a, b = synthetic.head_state(dim), weights.head_state(dim)
+        assert all(np.array_equal(a[k], b[k]) for k in b)
+    assert np.array_equal(synthetic.structured_images(2, 64, 96, seed=2001), data.structured_images(2, 64, 96, seed=2001))
