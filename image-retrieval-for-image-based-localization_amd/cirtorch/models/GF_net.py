@@ -194,46 +194,115 @@ def _to_tensor(img):
     return torch.from_numpy(a.transpose(2, 0, 1).copy())
 
 
-def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], msp=1, print_freq=10):
+def _decode(item, image_size, bbx, transform, tf):
+    """one input -> CHW tensor on the host: uint8 pixels (no transform) or the
+    transform's float tensor."""
+    if not isinstance(item, str):
+        return item
+    if tf is not None:                       # ISSTestTransform semantics (bbx crop, shortest side)
+        from PIL import Image
+        with open(item, "rb") as f:
+            pil = Image.open(f).convert("RGB")
+        return tf.pixels(pil, bbx) if transform is None else transform(tf._resized(pil, bbx))
+    pil = _load_pil(item, image_size, bbx)
+    # no transform: the decoded uint8 pixels cross PCIe (1 B per channel) and the
+    # fused stem reads them as x / 255 (== _to_tensor, bit for bit)
+    return transform(pil) if transform is not None else _to_pixels(pil)
+
+
+def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], msp=1, print_freq=10,
+                    batch=64, workers=8, test_transform=None):
     """Upstream ``extract_vectors`` (``scripts/test.py:200,236-238``): returns a
-    CPU float32 tensor D x len(images).  ``images`` are file paths (loaded with
-    PIL, longest side resized to image_size) or [3, H, W] tensors in [0, 1].
-    ms/msp follow the upstream rule: v = (mean_s f(x_s)^msp)^(1/msp), L2N."""
+    CPU float32 tensor D x len(images).  ``images`` are file paths (PIL load,
+    bbx crop, longest side resized to image_size — or ``test_transform``, an
+    ``ISSTestTransform`` of the in-tree loaders) or [3, H, W] tensors (float
+    in [0, 1] or uint8 pixels).  ms/msp follow the upstream rule:
+    v = (mean_s f(x_s)^msp)^(1/msp), then L2-normalised.
+
+    Each image is extracted on its own, as with batch size 1: images are
+    grouped by size (nothing is ever padded inside a group) into chains of up
+    to ``batch`` images.  Windows of ``8 * batch`` inputs are decoded by
+    ``workers`` host threads while the GPU extracts the previous window;
+    groups travel as pinned uint8 pixels on a copy stream double-buffered
+    against the extractor (the fused stem reads x / 255)."""
+    from concurrent.futures import ThreadPoolExecutor
     dev = next(net.parameters()).device
-    vecs = torch.zeros(net.meta.get("outputdim", 2048), len(images))
+    n = len(images)
+    D = net.meta.get("outputdim", 2048)
+    vecs = torch.zeros(D, n, device=dev)
+    if n == 0:
+        return vecs.cpu()
     normalize_in_net = net.augment is not None and transform is None
-    for i, item in enumerate(images):
-        if isinstance(item, str):
-            pil = _load_pil(item, image_size, bbxs[i] if bbxs is not None else None)
-            # no transform: the decoded uint8 pixels cross PCIe (1 B per channel) and
-            # the fused stem reads them as x / 255 (== _to_tensor, bit for bit)
-            x = transform(pil) if transform is not None else _to_pixels(pil)
+    mean = torch.tensor(net.meta["mean"], device=dev)[:, None, None] if net.meta.get("mean") is not None else None
+    std = torch.tensor(net.meta["std"], device=dev)[:, None, None] if net.meta.get("std") is not None else None
+    ms = list(ms)
+    main = torch.cuda.current_stream(dev)
+    copy = torch.cuda.Stream(dev)
+    pinned = {}
+    copied = [torch.cuda.Event(), torch.cuda.Event()]
+    freed = [torch.cuda.Event(), torch.cuda.Event()]
+    for e in freed:
+        e.record(main)
+    state = {"slot": 0}
+
+    def run(part, items):
+        """one same-size group of images -> their descriptor columns"""
+        slot = state["slot"]
+        if len(part) > 1:
+            key = (slot, len(part), tuple(items[0].shape), items[0].dtype)
+            host = pinned.get(key)
+            if host is None:
+                host = pinned[key] = torch.empty((len(part),) + tuple(items[0].shape), dtype=items[0].dtype).pin_memory()
+            copied[slot].synchronize()        # the previous H2D out of this host buffer has finished
+            torch.stack(items, out=host)
         else:
-            x = item
-        x = x.to(dev)
-        if x.dtype == torch.uint8 and (list(ms) != [1] or not normalize_in_net):
+            host = items[0][None]
+        copy.wait_event(freed[slot])          # the extractor is done with this slot's device buffer
+        with torch.cuda.stream(copy):
+            x = host.to(dev, non_blocking=len(part) > 1)
+        copied[slot].record(copy)
+        main.wait_event(copied[slot])
+        x.record_stream(main)
+        if x.dtype == torch.uint8 and (ms != [1] or not normalize_in_net):
             x = _ops.pixels_to_unit(x)
         elif x.dtype != torch.uint8:
             x = x.float()
-        if not normalize_in_net and transform is None and net.meta.get("mean") is not None:
-            m = torch.tensor(net.meta["mean"], device=dev)[:, None, None]
-            s = torch.tensor(net.meta["std"], device=dev)[:, None, None]
-            x = (x - m) / s
-        saved = net.augment
-        if not normalize_in_net:
-            net.augment = None
-        try:
-            if list(ms) == [1]:
-                v = net.extract(x[None] if x.dtype == torch.uint8 else [x])[:, 0]
-            else:
-                acc = None
-                for s in ms:
-                    xs = x if s == 1 else _ops.resize_bilinear(x, s)
-                    v = net.extract([xs])[:, 0].pow(msp)
-                    acc = v if acc is None else acc + v
-                v = (acc / len(ms)).pow(1.0 / msp)
-                v = v / v.norm()
-        finally:
-            net.augment = saved
-        vecs[:, i] = v.float().cpu()
-    return vecs
+        if not normalize_in_net and transform is None and mean is not None:
+            x = (x - mean) / std
+        if ms == [1]:
+            v = net.extract(x)
+        else:
+            acc = None
+            for s in ms:
+                xs = x if s == 1 else _ops.resize_bilinear(x, s)
+                vs = net.extract(xs).pow(msp)
+                acc = vs if acc is None else acc + vs
+            v = (acc / len(ms)).pow(1.0 / msp)
+            v = v / v.norm(dim=0, keepdim=True)
+        vecs[:, torch.tensor(part, device=dev)] = v.float()
+        freed[slot].record(main)
+        state["slot"] = slot ^ 1
+
+    saved = net.augment
+    if not normalize_in_net:
+        net.augment = None
+    win = max(1, 8 * batch)
+    try:
+        with ThreadPoolExecutor(max_workers=max(1, workers)) as pool, torch.no_grad():
+            def submit(w0):
+                return [pool.submit(_decode, images[i], image_size, bbxs[i] if bbxs is not None else None,
+                                    transform, test_transform) for i in range(w0, min(n, w0 + win))]
+            pending = submit(0)
+            for w0 in range(0, n, win):
+                decoded = [f.result() for f in pending]
+                pending = submit(w0 + win) if w0 + win < n else []
+                groups = {}
+                for j, x in enumerate(decoded):
+                    groups.setdefault((tuple(x.shape), x.dtype), []).append(j)
+                for js in groups.values():
+                    for b0 in range(0, len(js), batch):
+                        sub = js[b0:b0 + batch]
+                        run([w0 + j for j in sub], [decoded[j] for j in sub])
+    finally:
+        net.augment = saved
+    return vecs.cpu()

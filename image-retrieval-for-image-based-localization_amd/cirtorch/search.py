@@ -117,14 +117,18 @@ def shard_range(n, rank, world):
 
 
 def all_gather_stacked(t, group=None):
-    """[...] per rank -> [R, ...] on every rank (RCCL all-gather on GPU tensors)."""
+    """[...] per rank -> [R, ...] on every rank.  GPU tensors on an RCCL group
+    ("nccl" backend on ROCm): one all_gather_into_tensor over xGMI.  Other
+    backends (gloo) gather host copies and the result returns to t's device."""
     world = dist.get_world_size(group)
-    out = torch.empty((world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
-    if t.is_cuda:
+    if t.is_cuda and dist.get_backend(group) == "nccl":
+        out = torch.empty((world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
         dist.all_gather_into_tensor(out, t.contiguous(), group=group)
-    else:
-        dist.all_gather(list(out.unbind(0)), t.contiguous(), group=group)
-    return out
+        return out
+    host = t.detach().cpu().contiguous()
+    out = torch.empty((world,) + tuple(host.shape), dtype=host.dtype)
+    dist.all_gather(list(out.unbind(0)), host, group=group)
+    return out.to(t.device)
 
 
 class ShardedIndex:

@@ -6,6 +6,7 @@ database and query vector — runs on the GPU engine: Y = P[:d] (X - m), then
 column L2 normalisation with +1e-6 on the norm (``whiten.py:10``)."""
 
 import os
+import sys
 
 import numpy as np
 import torch
@@ -26,6 +27,12 @@ def whitenapply(X, m, P, dimensions=None):
     dev = Xt.device if Xt.is_cuda else torch.device("cuda")
     rows = Xt.t().to(dev).float().contiguous()                                    # [N, D]
     mt = torch.as_tensor(np.asarray(m) if not torch.is_tensor(m) else m).to(dev).double().reshape(-1)
+    if not torch.is_tensor(P) and np.iscomplexobj(P):
+        # np.linalg.eig of a numerically non-symmetric D can return a negligible
+        # imaginary part; a real one means degenerate training pairs
+        if np.abs(P.imag).max() > 1e-9 * max(np.abs(P.real).max(), 1e-300):
+            raise ValueError("whitenapply: complex whitening matrix (degenerate whitenlearn input)")
+        P = P.real
     Pt = torch.as_tensor(np.asarray(P) if not torch.is_tensor(P) else P).to(dev).double()
     y = _ops.whitenapply_rows(rows, mt, Pt, int(dimensions))                       # [N, d]
     Y = y.t()
@@ -70,4 +77,4 @@ def cholesky(S):
         except np.linalg.LinAlgError:
             alpha = 1e-10 if alpha == 0 else alpha * 10
             print(">>>> {}::cholesky: Matrix is not positive definite, adding {:.0e} on the diagonal"
-                  .format(os.path.basename(__file__), alpha))
+                  .format(os.path.basename(__file__), alpha), file=sys.stderr)

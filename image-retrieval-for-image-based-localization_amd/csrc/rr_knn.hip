@@ -516,8 +516,11 @@ int rr_knn_topk(const void* db, const float* db_f32, long long n_db, const void*
     }
 
     const size_t esz = dtype == RR_F32 ? 4 : 2;
-    // a kernel, not hipMemsetAsync: the reset must replay as an ordered node of a captured hipGraph
-    hipLaunchKernelGGL(k_zero_u32, dim3((nq + 255) / 256), dim3(256), 0, s, tau, nq);
+    // the running threshold is reset by a kernel (RR_KNN_TAU_MEMSET=1: by
+    // hipMemsetAsync, kept to reproduce the graph-replay finding of DESIGN §4)
+    static const bool tau_memset = getenv("RR_KNN_TAU_MEMSET") && getenv("RR_KNN_TAU_MEMSET")[0] == '1';
+    if (tau_memset) (void)hipMemsetAsync(tau, 0, (size_t)nq * 4, s);
+    else hipLaunchKernelGGL(k_zero_u32, dim3((nq + 255) / 256), dim3(256), 0, s, tau, nq);
     for (long long r0 = 0; r0 < n_db; r0 += (long long)p.G * p.L) {
         const int rows = (int)((n_db - r0) < (long long)p.G * p.L ? (n_db - r0) : (long long)p.G * p.L);
         ConvArgs a{};

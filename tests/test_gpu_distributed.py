@@ -1,0 +1,76 @@
+"""Sharded matching with the REAL kernels across processes (gloo, world 2 and
+3, every rank on cuda:0): per-shard HIP KnnIndex search, all-gather of the
+(score, index) lists through host copies, HIP rr_topk_merge — bit-identical
+to one search of the whole database (the reference never gathers: scripts/
+train_globalF.py:652-657,678,720).  World 3 with a 2-row database leaves one
+rank with an empty shard, which must contribute sentinels instead of hanging
+the gather."""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n, d, q, k, prec, ret):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.join(os.path.dirname(here), "image-retrieval-for-image-based-localization_amd"),
+              os.path.dirname(here)):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from cirtorch import _ops
+        from cirtorch.search import ShardedIndex, shard_range, all_gather_stacked
+        dev = torch.device("cuda", 0)
+        r0, nl = shard_range(n, rank, world)
+        db = _ops.fill_unit_rows(n, d, seed=0x5EED1, device=dev)[r0:r0 + nl].contiguous()
+        idx = ShardedIndex(db, r0, precision=prec)
+        # each rank extracts its own queries, then all of them are gathered (bench.py step)
+        qs = _ops.fill_unit_rows(q * world, d, seed=0x5EED2, device=dev)[rank * q:(rank + 1) * q].contiguous()
+        qa = all_gather_stacked(qs).reshape(world * q, d)
+        s, i = idx.search(qa, k)
+        torch.cuda.synchronize()
+        ret[rank] = (s.cpu().numpy(), i.cpu().numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n,prec", [(2, 30000, "bf16"), (2, 20011, "fp16"), (3, 2, "fp32")])
+def test_sharded_real_kernels_equal_single_search(cuda, world, n, prec):
+    from cirtorch import _ops
+    from cirtorch.search import KnnIndex
+    d, q, k = 256, 3, 50
+    ctx = mp.get_context("spawn")
+    mgr = ctx.Manager()
+    ret = mgr.dict()
+    mp.start_processes(_worker, args=(world, _free_port(), n, d, q, k, prec, ret), nprocs=world, join=True,
+                       start_method="spawn")
+    db = _ops.fill_unit_rows(n, d, seed=0x5EED1, device=cuda)
+    qa = _ops.fill_unit_rows(q * world, d, seed=0x5EED2, device=cuda)
+    s1, i1 = KnnIndex(db, prec).search(qa, k)
+    s1, i1 = s1.cpu().numpy(), i1.cpu().numpy()
+    for r in range(world):
+        s, i = ret[r]
+        np.testing.assert_array_equal(i, i1)
+        np.testing.assert_array_equal(s, s1)
+    if n < k:
+        assert (i1[:, n:] == -1).all()

@@ -114,3 +114,66 @@ def test_extract_vectors_uint8_files_equal_float_tensors(cuda, tmp_path):
         a = extract_vectors(net, paths, 128)
         b = extract_vectors(net, [_to_tensor(_load_pil(p, 128)) for p in paths], 128)
         assert torch.equal(a, b), prec
+
+
+def _write_pngs(tmp_path, n_distinct, h, w, copies, seed):
+    from PIL import Image
+    from oracle import data
+    paths = []
+    for i, im in enumerate(data.structured_images(n_distinct, h, w, seed=seed)):
+        arr = (np.clip(im.transpose(1, 2, 0), 0, 1) * 255).astype(np.uint8)
+        p = os.path.join(str(tmp_path), "b%d.png" % i)
+        Image.fromarray(arr).save(p, compress_level=1)
+        paths.append(p)
+    return [paths[i % n_distinct] for i in range(n_distinct * copies)]
+
+
+@pytest.mark.parametrize("prec", ["fp16", "fp32"])
+def test_extract_vectors_batched_equals_batch1(cuda, tmp_path, prec):
+    """extract_vectors groups same-size images into chains (pinned uint8
+    pixels, copy stream double-buffered against the extractor); every column
+    equals the batch-1 extraction of that image (one call per file) up to the
+    kernel variant the chain size selects (fp32: one kernel family, identical)."""
+    from cirtorch.models.GF_net import extract_vectors, make_net
+    from cirtorch.models.init import random_init_
+    net = make_net("resnet50", precision=prec, mean=MEAN, std=STD)
+    random_init_(net, seed=6)
+    net = net.to(cuda).eval()
+    paths = _write_pngs(tmp_path, 6, 240, 320, 4, seed=71)          # 24 same-size files
+    other = tmp_path / "other"
+    other.mkdir()
+    paths.insert(5, _write_pngs(other, 1, 200, 300, 1, seed=72)[0])    # one image of another size
+    vecs = extract_vectors(net, paths, None, batch=8, workers=4)
+    one = torch.cat([extract_vectors(net, [p], None) for p in paths[:9]], dim=1)
+    d = (vecs[:, :9] - one).abs().max().item()
+    print(prec, "batched vs batch-1 max |d|", d)
+    assert cosines(vecs[:, :9].numpy(), one.numpy()).min() > 1 - 1e-6
+    if prec == "fp32":
+        assert d < 1e-6
+    # the same file appears several times: identical columns
+    assert torch.equal(vecs[:, 0], vecs[:, 6 + 1])
+
+
+def test_extract_vectors_iss_test_transform(cuda, tmp_path):
+    """test_transform=ISSTestTransform: the in-tree loaders' resize rule (shortest
+    side -> shortest_size, longest capped) feeds the engine as uint8 pixels;
+    equal to extracting the transform's float output."""
+    from PIL import Image
+    from cirtorch.datasets.generic import ISSTestTransform
+    from cirtorch.models.GF_net import extract_vectors, make_net
+    from cirtorch.models.init import random_init_
+    net = make_net("resnet18", precision="fp16", mean=MEAN, std=STD)
+    random_init_(net, seed=8)
+    net = net.to(cuda).eval()
+    paths = _write_pngs(tmp_path, 3, 150, 210, 1, seed=81)
+    tf = ISSTestTransform(shortest_size=96, longest_max_size=128, random_scale=[0.8, 1.2])
+    bbxs = [None, (5, 10, 180, 140), None]
+    a = extract_vectors(net, paths, None, bbxs=bbxs, test_transform=tf)
+    imgs = []
+    for p, b in zip(paths, bbxs):
+        with open(p, "rb") as f:
+            imgs.append(tf(Image.open(f).convert("RGB"), bbx=b)["img"])
+    b_ = extract_vectors(net, imgs, None)
+    assert torch.equal(a, b_)
+    assert tuple(imgs[0].shape[1:]) == tf.output_size(210, 150)[::-1] == (91, 128)
+    assert tuple(imgs[1].shape[1:]) == tf.output_size(175, 130)[::-1]
