@@ -245,7 +245,7 @@ def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], 
         e.record(main)
     state = {"slot": 0}
 
-    def run(part, items):
+    def run(part, items, pool):
         """one same-size group of images -> their descriptor columns"""
         slot = state["slot"]
         if len(part) > 1:
@@ -254,7 +254,8 @@ def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], 
             if host is None:
                 host = pinned[key] = torch.empty((len(part),) + tuple(items[0].shape), dtype=items[0].dtype).pin_memory()
             copied[slot].synchronize()        # the previous H2D out of this host buffer has finished
-            torch.stack(items, out=host)
+            # gather into the pinned buffer on the worker threads (tensor copies release the GIL)
+            list(pool.map(lambda j: host[j].copy_(items[j]), range(len(part))))
         else:
             host = items[0][None]
         copy.wait_event(freed[slot])          # the extractor is done with this slot's device buffer
@@ -288,7 +289,8 @@ def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], 
         net.augment = None
     win = max(1, 8 * batch)
     try:
-        with ThreadPoolExecutor(max_workers=max(1, workers)) as pool, torch.no_grad():
+        with ThreadPoolExecutor(max_workers=max(1, workers)) as pool, \
+                ThreadPoolExecutor(max_workers=max(1, workers)) as cpool, torch.no_grad():
             def submit(w0):
                 return [pool.submit(_decode, images[i], image_size, bbxs[i] if bbxs is not None else None,
                                     transform, test_transform) for i in range(w0, min(n, w0 + win))]
@@ -302,7 +304,7 @@ def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], 
                 for js in groups.values():
                     for b0 in range(0, len(js), batch):
                         sub = js[b0:b0 + batch]
-                        run([w0 + j for j in sub], [decoded[j] for j in sub])
+                        run([w0 + j for j in sub], [decoded[j] for j in sub], cpool)
     finally:
         net.augment = saved
     return vecs.cpu()
