@@ -439,7 +439,7 @@ namespace rr {
 void set_gemm_tuning(int key, int value);
 }
 extern "C" int rr_set_tuning(int key, int value) {
-    if (key < 0 || key > 7) return fail(RR_EINVAL, "rr_set_tuning: unknown key");
+    if (key < 0 || key > 8) return fail(RR_EINVAL, "rr_set_tuning: unknown key");
     if (key == RR_TUNE_GRID_CUS) {
         if (value < 0) return fail(RR_EINVAL, "rr_set_tuning: RR_TUNE_GRID_CUS must be >= 0");
         rr::g_grid_cap = value;

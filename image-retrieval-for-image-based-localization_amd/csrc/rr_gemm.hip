@@ -583,6 +583,353 @@ static void launch_cfg3(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
     launch_ns<T, TO, TC, TP, WC, WP, 2>(a, k1, perm, s);
 }
 
+
+// ---------------------------------------------------------------------------
+// 8-phase 256 x 256 tile with staggered wave groups (16-bit operands).
+//
+// The k_igemm ring above keeps ONE K-step in flight across each barrier pair,
+// so every 64-deep step waits on its own LDS-DMA (MFMA busy ~40 %).  Here the
+// 256 x 256 x 64 step is split into four 128 x 128 quadrants and the operand
+// tiles into half-tiles (A0 / A1 = channel rows 0-127 / 128-255, B0 / B1 =
+// pixel rows 0-127 / 128-255; 128 rows x 128 B = 16 KiB each), double
+// buffered (E: even K-steps, O: odd; 128 KiB of LDS):
+//   * a phase = one quadrant x K 64: the block's 8 waves each do a 64 x 32
+//     sub-block (16 MFMAs), reading only the half-tiles of that quadrant;
+//     quadrant order (0,0) (0,1) (1,1) (1,0) reuses the A or B fragments of
+//     the previous phase from registers;
+//   * every phase issues ONE half-tile LDS-DMA (2 per lane), into the
+//     half-tile whose last read was two phases earlier, for the K-step that
+//     buffer holds next: each load has 4-7 phases to land;
+//   * s_waitcnt vmcnt(4) once per K-step (phases 4 and 8) retires the loads
+//     the next four phases read; raw s_barrier, never vmcnt(0) in the loop;
+//   * waves 4-7 run one barrier behind waves 0-3 (each SIMD holds one wave
+//     of each group): while one group runs its MFMA cluster the other reads
+//     LDS / issues DMA, so the matrix pipe of every SIMD alternates between
+//     two instruction streams.  The two-phase restage distance and the wait
+//     placement (before the first barrier of the phase preceding the reads)
+//     are what keep both hazards closed under that one-barrier skew.
+// Tiles are assigned XCD-contiguously (bijective remap): the pixel tiles of
+// one channel tile (e.g. the query tiles of one database tile in the kNN
+// score GEMM) share their A rows in one XCD's L2.  One tile per block.
+template <typename T, typename TO, int KM, bool PERM>
+__global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int ntiles) {
+    static_assert(sizeof(T) == 2, "16-bit operands");
+    constexpr bool K1 = KM == 1, tapu = KM == 2;
+    constexpr int VEC = 8, ESZ = 2, HT = 16384;
+    __shared__ __attribute__((aligned(1024))) char smem[8 * HT];  // [buf E/O][A0, A1, B0, B1]
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wave >> 2;              // wave group; also the 64-row half of each quadrant
+    const int wn = wave & 3;                // 32-column quarter of each quadrant
+    // XCD-contiguous bijective tile order (blocks are dispatched round-robin over 8 XCDs)
+    const int nwg = (int)gridDim.x, bx = (int)blockIdx.x;
+    const int xcd = bx & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bx >> 3);
+    if (t >= ntiles) return;
+    const int c0 = (t / tiles_p) * 256, p0 = (t % tiles_p) * 256;
+    const int H = a.h, W = a.w_, Cin = a.cin;
+    const int nk = a.kp / 64;
+    const unsigned lds0 = (unsigned)(unsigned long long)smem;
+    const int lrow = lane >> 3, lchunk = (lane & 7) ^ (lrow & 7);
+
+    // ---- LDS-DMA descriptors: half-tile h, instruction i covers rows (wave + 8 i) * 8 + lrow
+    const long long arows = min(256, a.cout - c0);
+    const i32x4_t rsA = make_rsrc((const char*)a.w + (long long)c0 * a.kp * ESZ, (unsigned)(arows * a.kp * ESZ));
+    const i32x4_t rsB = make_rsrc(a.x, (unsigned)((long long)a.n * H * W * Cin * ESZ));
+    unsigned a_off[2][2], b_base[2][2];
+    int b_hi[2][2], b_wi[2][2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int row = h * 128 + (wave + 8 * i) * 8 + lrow;
+            a_off[h][i] = row < arows ? (unsigned)(((long long)row * a.kp + lchunk * VEC) * ESZ) : OOB;
+            const int p = p0 + row;
+            if (p < a.P) {
+                const int img = p / (a.ho * a.wo);
+                const int rem = p - img * (a.ho * a.wo);
+                const int oh = rem / a.wo, ow = rem - oh * a.wo;
+                b_hi[h][i] = oh * a.stride - a.pad;
+                b_wi[h][i] = ow * a.stride - a.pad;
+                b_base[h][i] = (unsigned)((long long)img * H * W * Cin + ((long long)b_hi[h][i] * W + b_wi[h][i]) * Cin +
+                                          lchunk * VEC);
+            } else {
+                b_hi[h][i] = b_wi[h][i] = -(1 << 28);
+                b_base[h][i] = OOB;
+            }
+        }
+    // half-tile X (0 A0, 1 A1, 2 B0, 3 B1) of K-step kt into buffer buf; K-steps >= nk load zeros
+    auto issue = [&](int X, int kt, int buf) {
+        const unsigned dst = lds0 + (buf * 4 + X) * HT;
+        const bool live = kt < nk;
+        if (X < 2) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const unsigned off = (live && a_off[X][i] != OOB) ? a_off[X][i] + (unsigned)(kt * 128) : OOB;
+                dma16(rsA, off, dst + (wave + 8 * i) * 1024);
+            }
+        } else {
+            const int h = X - 2, k0 = kt * 64;
+            int tap_dh = 0, tap_dw = 0, tap_add = 0;
+            if constexpr (tapu) {
+                const int tap = k0 >> a.lc, ci0 = k0 & (Cin - 1);
+                const int kh = tap / a.kw, kw = tap - kh * a.kw;
+                tap_dh = kh * a.dil;
+                tap_dw = kw * a.dil;
+                tap_add = (tap_dh * W + tap_dw) * Cin + ci0;
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                unsigned off = OOB;
+                if (live && b_base[h][i] != OOB) {
+                    if constexpr (K1) {
+                        off = (b_base[h][i] + (unsigned)k0) * ESZ;
+                    } else {
+                        const int hi = b_hi[h][i] + tap_dh, wi = b_wi[h][i] + tap_dw;
+                        if ((unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W)
+                            off = (b_base[h][i] + (unsigned)tap_add) * ESZ;
+                    }
+                }
+                dma16(rsB, off, dst + (wave + 8 * i) * 1024);
+            }
+        }
+    };
+
+    f32x4_t acc[2][2][4][2];
+#pragma unroll
+    for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[qa][qb][i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+    const int r16 = lane & 15, kq = lane >> 4;
+    uint4 fa[4][2], fb[2][2];
+    auto read_a = [&](int buf, int h) {
+        const char* base = smem + (buf * 4 + h) * HT;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int hs = 0; hs < 2; ++hs)
+                fa[i][hs] = *reinterpret_cast<const uint4*>(base + swz(grp * 64 + i * 16 + r16, kq + 4 * hs));
+    };
+    auto read_b = [&](int buf, int h) {
+        const char* base = smem + (buf * 4 + 2 + h) * HT;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int hs = 0; hs < 2; ++hs)
+                fb[j][hs] = *reinterpret_cast<const uint4*>(base + swz(wn * 32 + j * 16 + r16, kq + 4 * hs));
+    };
+    auto mfma_q = [&](int qa, int qb) {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int hs = 0; hs < 2; ++hs)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    if constexpr (std::is_same<T, f16_t>::value)
+                        acc[qa][qb][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                            __builtin_bit_cast(f16x8_t, fa[i][hs]), __builtin_bit_cast(f16x8_t, fb[j][hs]),
+                            acc[qa][qb][i][j], 0, 0, 0);
+                    else
+                        acc[qa][qb][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                            __builtin_bit_cast(bf16x8_t, fa[i][hs]), __builtin_bit_cast(bf16x8_t, fb[j][hs]),
+                            acc[qa][qb][i][j], 0, 0, 0);
+                }
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto bar = []() { asm volatile("s_barrier" ::: "memory"); };
+
+    // ---- prologue: K-step 0 into E (A0 B1 A1 B0), K-step 1's A0 / B1 into O
+    issue(0, 0, 0);
+    issue(3, 0, 0);
+    issue(1, 0, 0);
+    issue(2, 0, 0);
+    issue(0, 1, 1);
+    issue(3, 1, 1);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    bar();
+    if (grp == 1) bar();  // stagger: group 1 runs one barrier behind group 0
+
+    const int nit = (nk + 1) >> 1;
+    for (int it = 0; it < nit; ++it) {
+        const int te = 2 * it, to = 2 * it + 1;
+        // phases 1-4: K-step te from E; loads: A1-O(to), B0-O(to), A0-E(te+2), B1-E(te+2)
+        read_a(0, 0); read_b(0, 0); issue(1, to, 1);
+        bar(); mfma_q(0, 0); bar();
+        read_b(0, 1); issue(2, to, 1);
+        bar(); mfma_q(0, 1); bar();
+        read_a(0, 1); issue(0, te + 2, 0);
+        bar(); mfma_q(1, 1); bar();
+        read_b(0, 0); issue(3, te + 2, 0);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // K-step `to` (buffer O) has landed
+        bar(); mfma_q(1, 0); bar();
+        // phases 5-8: K-step to from O; loads: A1-E(te+2), B0-E(te+2), A0-O(to+2), B1-O(to+2)
+        read_a(1, 0); read_b(1, 0); issue(1, te + 2, 0);
+        bar(); mfma_q(0, 0); bar();
+        read_b(1, 1); issue(2, te + 2, 0);
+        bar(); mfma_q(0, 1); bar();
+        read_a(1, 1); issue(0, to + 2, 1);
+        bar(); mfma_q(1, 1); bar();
+        read_b(1, 0); issue(3, to + 2, 1);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // K-step te + 2 (buffer E) has landed
+        bar(); mfma_q(1, 0); bar();
+    }
+    if (grp == 0) bar();  // equal barrier counts for both groups
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the block
+
+    // ---- epilogue: folded BN scale / shift, residual, activation, NHWC store
+    TO* __restrict__ Y = (TO*)a.y;
+    const TO* __restrict__ R = (const TO*)a.res;
+    const bool affine = a.flags & RR_CONV_AFFINE;
+    const bool resid = a.flags & RR_CONV_RESIDUAL;
+    const bool leaky = a.act == RR_ACT_LEAKY;
+#pragma unroll
+    for (int qa = 0; qa < 2; ++qa) {
+        if constexpr (PERM) {
+#pragma unroll
+            for (int i2 = 0; i2 < 2; ++i2) {
+                const int c = c0 + qa * 128 + grp * 64 + 32 * i2 + 8 * kq;  // 8 consecutive channels
+                if (c >= a.cout) continue;
+                float sc[8], sh[8];
+                if (affine) {
+                    St4<float>::ld(a.scale + c, sc);
+                    St4<float>::ld(a.scale + c + 4, sc + 4);
+                    St4<float>::ld(a.shift + c, sh);
+                    St4<float>::ld(a.shift + c + 4, sh + 4);
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) { sc[r] = 1.f; sh[r] = 0.f; }
+                }
+#pragma unroll
+                for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        const int p = p0 + qb * 128 + wn * 32 + j * 16 + r16;
+                        if (p >= a.P) continue;
+                        float v[8];
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            v[r] = acc[qa][qb][2 * i2][j][r] * sc[r] + sh[r];
+                            v[4 + r] = acc[qa][qb][2 * i2 + 1][j][r] * sc[4 + r] + sh[4 + r];
+                        }
+                        const long long o = (long long)p * a.ldy + c;
+                        if (resid) {
+                            float rv[8];
+                            St4<TO>::ld(R + o, rv);
+                            St4<TO>::ld(R + o + 4, rv + 4);
+#pragma unroll
+                            for (int r = 0; r < 8; ++r) v[r] += rv[r];
+                        }
+                        if (leaky) {
+#pragma unroll
+                            for (int r = 0; r < 8; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * a.slope;
+                        }
+                        if constexpr (sizeof(TO) == 2) {
+                            uint4 q;
+                            q.x = H16<TO>::pack2(v[0], v[1]);
+                            q.y = H16<TO>::pack2(v[2], v[3]);
+                            q.z = H16<TO>::pack2(v[4], v[5]);
+                            q.w = H16<TO>::pack2(v[6], v[7]);
+                            *reinterpret_cast<uint4*>(Y + o) = q;
+                        } else {
+                            St4<TO>::st(Y + o, v);
+                            St4<TO>::st(Y + o + 4, v + 4);
+                        }
+                    }
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int c = c0 + qa * 128 + grp * 64 + i * 16 + 4 * kq;
+                if (c >= a.cout) continue;
+                float sc[4] = {1.f, 1.f, 1.f, 1.f}, sh[4] = {0.f, 0.f, 0.f, 0.f};
+                const bool full = c + 3 < a.cout;
+                if (affine) {
+                    for (int r = 0; r < 4; ++r)
+                        if (c + r < a.cout) { sc[r] = a.scale[c + r]; sh[r] = a.shift[c + r]; }
+                }
+#pragma unroll
+                for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        const int p = p0 + qb * 128 + wn * 32 + j * 16 + r16;
+                        if (p >= a.P) continue;
+                        float v[4];
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) v[r] = acc[qa][qb][i][j][r] * sc[r] + sh[r];
+                        const long long o = (long long)p * a.ldy + c;
+                        if (full) {
+                            if (resid) {
+                                float rv[4];
+                                St4<TO>::ld(R + o, rv);
+#pragma unroll
+                                for (int r = 0; r < 4; ++r) v[r] += rv[r];
+                            }
+                            if (leaky) {
+#pragma unroll
+                                for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * a.slope;
+                            }
+                            St4<TO>::st(Y + o, v);
+                        } else {
+                            for (int r = 0; r < 4; ++r) {
+                                if (c + r >= a.cout) break;
+                                float tt = v[r];
+                                if (resid) tt += DT<TO>::to_f(R[o + r]);
+                                if (leaky) tt = tt > 0.f ? tt : tt * a.slope;
+                                Y[o + r] = DT<TO>::from_f(tt);
+                            }
+                        }
+                    }
+            }
+        }
+    }
+}
+
+static int g_gemm8 = -1;  // rr_set_tuning(RR_TUNE_GEMM8) / RR_GEMM8: 0 off, 1 auto (default), 2 force where legal
+
+// 16-bit operands, 1x1 or tap-uniform im2col, an even number of 64-deep
+// K-steps, and enough 256 x 256 tiles to fill the chip.
+template <typename T, typename TO>
+static bool try_gemm8(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
+    if constexpr (sizeof(T) != 2) {
+        return false;
+    } else {
+        if (g_gemm8 < 0) {
+            const char* e = getenv("RR_GEMM8");
+            g_gemm8 = (e && e[0] == '0') ? 0 : 1;
+        }
+        if (!g_gemm8) return false;
+        const int km = k1 ? 1 : (a.cin * 2) % 128 == 0 ? 2 : 0;
+        const int nk = a.kp / 64;
+        if (km == 0 || nk < 2 || (nk & 1) || a.kp % 64) return false;
+        const int tiles_p = (a.P + 255) / 256, tiles_c = (a.cout + 255) / 256;
+        const long long ntiles = (long long)tiles_p * tiles_c;
+        if (g_gemm8 == 1 && (a.P < 256 || ntiles < 2 * grid_cus())) return false;
+        if (perm && a.cout % 32) return false;
+        const dim3 g((unsigned)ntiles), b(512);
+#define RR_G8(KMV, PV) hipLaunchKernelGGL((k_gemm8<T, TO, KMV, PV>), g, b, 0, s, a, tiles_p, (int)ntiles)
+        if constexpr (std::is_same<T, TO>::value) {
+            if (perm) {
+                if (km == 1) RR_G8(1, true);
+                else RR_G8(2, true);
+                return true;
+            }
+        }
+        if (km == 1) RR_G8(1, false);
+        else RR_G8(2, false);
+#undef RR_G8
+        return true;
+    }
+}
+
 int g_force_cfg = 0;  // rr_set_tuning(RR_TUNE_GEMM_CONFIG, ...)
 
 template <typename T, typename TO>
@@ -600,6 +947,7 @@ void launch_gemm2(const ConvArgs& a, bool k1, hipStream_t s) {
         case 8: launch_ns<T, TO, 128, 256, 2, 4, 3>(a, k1, perm, s); return;  // 8 waves, 3-stage ring (144 KiB)
         default: break;
     }
+    if (g_force_cfg == 0 && try_gemm8<T, TO>(a, k1, perm, s)) return;
     // A-stationary variants (single output-channel tile, short K)
     const int nk = a.kp / (sizeof(T) == 2 ? 64 : 32);
     if (g_force_cfg == 6 || (g_force_cfg == 0 && g_ast)) {
@@ -640,6 +988,7 @@ void set_gemm_tuning(int key, int value) {
     else if (key == RR_TUNE_GEMM_WIDE) g_wide = value != 0;
     else if (key == RR_TUNE_GEMM_ASTAT) g_ast = value != 0;
     else if (key == RR_TUNE_GEMM_XCD_MAP) g_xmap = value != 0;
+    else if (key == RR_TUNE_GEMM8) g_gemm8 = value < 0 ? 0 : value > 2 ? 2 : value;
 }
 
 template void launch_gemm2<bf16_t, bf16_t>(const ConvArgs&, bool, hipStream_t);

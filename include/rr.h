@@ -243,10 +243,12 @@ int rr_mutual_nn(const long long* nn12, int n1, const long long* nn21, int n2, l
  *                        1x8 / 1x4 waves for the c_in = 64 A-stationary form,
  *                        7 a 3-stage weight ring, 8 256-channel x 6x32 tiles
  *   RR_TUNE_GRID_CUS     cap on the CUs one persistent launch spreads over
- *                        (0 = all; e.g. half the chip for two concurrent streams) */
+ *                        (0 = all; e.g. half the chip for two concurrent streams)
+ *   RR_TUNE_GEMM8        0 off, 1 auto, 2 forced: the 8-phase staggered 256x256 GEMM for eligible
+ *                        16-bit 1x1 / tap-uniform convs and score GEMMs (default 1) */
 enum rr_tune_key { RR_TUNE_GEMM_CONFIG = 0, RR_TUNE_GEMM_STAGES = 1, RR_TUNE_GEMM_WIDE = 2,
                    RR_TUNE_GEMM_ASTAT = 3, RR_TUNE_GEMM_XCD_MAP = 4, RR_TUNE_STREAM_1X1 = 5,
-                   RR_TUNE_CONV3X3 = 6, RR_TUNE_GRID_CUS = 7 };
+                   RR_TUNE_CONV3X3 = 6, RR_TUNE_GRID_CUS = 7, RR_TUNE_GEMM8 = 8 };
 int rr_set_tuning(int key, int value);
 
 /* ----------------------------------------------------------- data helpers */

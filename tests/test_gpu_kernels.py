@@ -405,3 +405,63 @@ def test_conv_fp16_splits_large_batches(cuda):
         yi = _ops().conv2d_fused(x[i:i + 1].contiguous(), wp, 1, 1, 1, 0, 64, leaky=False)
         assert torch.equal(y[i:i + 1], yi)
     del x
+
+
+GEMM8_CASES = [
+    # 16-bit 1x1 / tap-uniform 3x3 shapes with an even number of 64-deep K-steps (ragged P, c_out)
+    (2, 128, 17, 19, 256, 1, 1, 0, True, True),     # K = 128: 2 K-steps (one loop iteration)
+    (1, 256, 23, 29, 512, 1, 1, 0, False, True),    # two channel tiles
+    (1, 1024, 21, 25, 256, 1, 1, 0, False, True),   # mod4 conv1 shape, 16 K-steps
+    (1, 512, 19, 21, 320, 1, 1, 0, True, False),    # partial channel tile (OOB weight rows)
+    (1, 256, 19, 23, 256, 3, 2, 1, False, True),    # strided 3x3, tap-uniform im2col, 36 K-steps
+    (1, 128, 14, 18, 128, 3, 1, 1, True, True),     # halo taps at every border, 18 K-steps
+]
+
+
+@pytest.mark.parametrize("case", GEMM8_CASES)
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+@pytest.mark.parametrize("perm", [True, False])
+def test_gemm8_forced_vs_float64(cuda, case, prec, perm):
+    """The 8-phase staggered 256x256 GEMM (rr_set_tuning(RR_TUNE_GEMM8, 2):
+    forced wherever structurally legal) against the float64 reference."""
+    from cirtorch import _engine as E
+    E.check(E.lib().rr_set_tuning(8, 2), "rr_set_tuning")
+    E.check(E.lib().rr_set_tuning(6, 0), "rr_set_tuning")   # no direct 3x3 kernel
+    E.check(E.lib().rr_set_tuning(5, 0), "rr_set_tuning")   # no streaming 1x1 kernel
+    try:
+        _check_conv(cuda, case, prec, perm)
+    finally:
+        E.lib().rr_set_tuning(8, 1)
+        E.lib().rr_set_tuning(6, 1)
+        E.lib().rr_set_tuning(5, 1)
+
+
+@pytest.mark.parametrize("shape", [(128, 48, 64, 1024, 256, 1, 1), (128, 24, 32, 2048, 512, 1, 1),
+                                   (128, 48, 64, 256, 256, 3, 2), (128, 24, 32, 512, 512, 3, 2)])
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_gemm8_bit_identical_to_tiled_engine(cuda, shape, prec):
+    """R50 128-image shapes (mod4 / mod5 conv1, strided 3x3): the 8-phase
+    kernel uses the same operand layout and K order as the 2-stage tiled
+    engine, so the outputs are bit-identical."""
+    from cirtorch import _engine as E
+    n, h, w, cin, cout, k, s = shape
+    g = torch.Generator(device=cuda).manual_seed(9)
+    dt = torch.bfloat16 if prec == "bf16" else torch.float16
+    x = torch.randn((n, h, w, cin), generator=g, device=cuda).to(dt)
+    wt = torch.randn((cout, cin, k, k), generator=g, device=cuda) * (2.0 / (cin * k * k)) ** 0.5
+    wp = _ops().pack_conv_weights(wt, cin, dt, perm32=True)
+    sc = torch.rand(cout, generator=g, device=cuda) + 0.5
+    sh = torch.randn(cout, generator=g, device=cuda) * 0.1
+    p = 1 if k == 3 else 0
+    E.check(E.lib().rr_set_tuning(6, 0), "rr_set_tuning")
+    E.check(E.lib().rr_set_tuning(5, 0), "rr_set_tuning")
+    E.check(E.lib().rr_set_tuning(8, 2), "rr_set_tuning")
+    try:
+        a = _ops().conv2d_fused(x, wp, k, k, s, p, cout, sc, sh, leaky=True, perm32=True)
+        E.check(E.lib().rr_set_tuning(8, 0), "rr_set_tuning")
+        b = _ops().conv2d_fused(x, wp, k, k, s, p, cout, sc, sh, leaky=True, perm32=True)
+    finally:
+        E.lib().rr_set_tuning(8, 1)
+        E.lib().rr_set_tuning(6, 1)
+        E.lib().rr_set_tuning(5, 1)
+    assert torch.equal(a, b)
