@@ -346,6 +346,8 @@ int g_conv3_mode = 1;  // rr_set_tuning(RR_TUNE_CONV3X3): 0 off, 1 auto, 2 / 3 p
 // bf16 3x3 / stride 1 / pad 1 with PERM32 weights, bf16 out, no residual, and
 // image sizes the tiles divide; returns false otherwise (caller falls back to
 // the implicit-GEMM engine).
+bool gemm8_eligible(const ConvArgs& a, bool k1, int esz);  // rr_gemm.hip
+
 bool launch_conv3x3(const ConvArgs& a, hipStream_t s, bool f16) {
     if (g_conv3_mode == 0) return false;
     if (a.kh != 3 || a.kw != 3 || a.stride != 1 || a.pad != 1 || a.dil != 1) return false;
@@ -353,6 +355,10 @@ bool launch_conv3x3(const ConvArgs& a, hipStream_t s, bool f16) {
     if (a.cin % 64 || a.kp != 9 * a.cin || a.w_ % 32) return false;
     if ((long long)a.n * a.h * a.w_ * a.cin * 2 >= (1ll << 31)) return false;
     if ((long long)a.n * a.h * a.w_ >= (1ll << 31) / 2) return false;
+    // 256-multiple output channels on a chip-filling problem (mod4 / mod5 3x3 at
+    // 128 images): the 8-phase GEMM on tap-uniform im2col beats the direct
+    // kernel (420 vs 479, 392 vs 455 us) — the taps re-read from L2
+    if (a.cout % 256 == 0 && g_conv3_mode == 1 && gemm8_eligible(a, false, 2)) return false;
     const int g_c3_cus = grid_cus();
     if (a.cin == 64 && a.cout == 64 && a.h % 8 == 0) {
         // 8 waves (2 per SIMD) measured fastest: 125 us vs 146 (4 waves) at 32 x 192x256x64

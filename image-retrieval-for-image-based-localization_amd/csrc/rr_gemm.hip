@@ -896,24 +896,34 @@ __global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int n
 static int g_gemm8 = -1;  // rr_set_tuning(RR_TUNE_GEMM8) / RR_GEMM8: 0 off, 1 auto (default), 2 force where legal
 
 // 16-bit operands, 1x1 or tap-uniform im2col, an even number of 64-deep
-// K-steps, and enough 256 x 256 tiles to fill the chip.
+// K-steps, 31-bit operand offsets, and (auto) enough 256 x 256 tiles to fill
+// the chip twice with no half-empty channel tile (c_out = 128 would waste
+// half the MFMAs).
+bool gemm8_eligible(const ConvArgs& a, bool k1, int esz) {
+    if (g_gemm8 < 0) {
+        const char* e = getenv("RR_GEMM8");
+        g_gemm8 = (e && e[0] == '0') ? 0 : 1;
+    }
+    if (!g_gemm8 || esz != 2) return false;
+    const int km = k1 ? 1 : (a.cin * 2) % 128 == 0 ? 2 : 0;
+    const int nk = a.kp / 64;
+    if (km == 0 || nk < 2 || (nk & 1) || a.kp % 64) return false;
+    if ((long long)a.n * a.h * a.w_ * a.cin * 2 >= (1ll << 31) || 256ll * a.kp * 2 >= (1ll << 31)) return false;
+    if ((a.flags & RR_CONV_PERM32) && a.cout % 32) return false;
+    const long long ntiles = (long long)((a.P + 255) / 256) * ((a.cout + 255) / 256);
+    if (g_gemm8 == 1 && (a.P < 256 || ntiles < 2 * grid_cus() || a.cout % 256)) return false;
+    return true;
+}
+
 template <typename T, typename TO>
 static bool try_gemm8(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
     if constexpr (sizeof(T) != 2) {
         return false;
     } else {
-        if (g_gemm8 < 0) {
-            const char* e = getenv("RR_GEMM8");
-            g_gemm8 = (e && e[0] == '0') ? 0 : 1;
-        }
-        if (!g_gemm8) return false;
-        const int km = k1 ? 1 : (a.cin * 2) % 128 == 0 ? 2 : 0;
-        const int nk = a.kp / 64;
-        if (km == 0 || nk < 2 || (nk & 1) || a.kp % 64) return false;
+        if (!gemm8_eligible(a, k1, 2)) return false;
+        const int km = k1 ? 1 : 2;
         const int tiles_p = (a.P + 255) / 256, tiles_c = (a.cout + 255) / 256;
         const long long ntiles = (long long)tiles_p * tiles_c;
-        if (g_gemm8 == 1 && (a.P < 256 || ntiles < 2 * grid_cus())) return false;
-        if (perm && a.cout % 32) return false;
         const dim3 g((unsigned)ntiles), b(512);
 #define RR_G8(KMV, PV) hipLaunchKernelGGL((k_gemm8<T, TO, KMV, PV>), g, b, 0, s, a, tiles_p, (int)ntiles)
         if constexpr (std::is_same<T, TO>::value) {
