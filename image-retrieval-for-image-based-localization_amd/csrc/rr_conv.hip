@@ -297,6 +297,7 @@ static void launch(const ConvArgs& a, bool k1, hipStream_t s) {
 }
 
 template <typename T, typename TO> void launch_gemm2(const ConvArgs& a, bool k1, hipStream_t s);
+extern int g_knn_fused;  // rr_knn.hip
 bool launch_stream1x1(const ConvArgs& a, hipStream_t s, bool f16);  // rr_stream.hip
 bool launch_conv3x3(const ConvArgs& a, hipStream_t s, bool f16);    // rr_conv3.hip
 extern int g_stream_mode;
@@ -393,7 +394,7 @@ extern "C" int rr_conv2d_fused(const void* x, const void* w, const float* scale,
         d->wo != (d->w + 2 * d->pad - d->dil * (d->kw - 1) - 1) / d->stride + 1)
         return fail(RR_EINVAL, "rr_conv2d_fused: output size inconsistent with kernel/stride/pad");
 
-    ConvArgs a;
+    ConvArgs a{};
     a.x = x; a.w = w; a.scale = scale; a.shift = shift; a.res = residual; a.y = y;
     a.n = d->n; a.h = d->h; a.w_ = d->w; a.cin = d->c_in; a.ho = d->ho; a.wo = d->wo; a.cout = d->c_out;
     a.kh = d->kh; a.kw = d->kw; a.stride = d->stride; a.pad = d->pad; a.dil = d->dil; a.kp = d->k_packed;
@@ -439,7 +440,11 @@ namespace rr {
 void set_gemm_tuning(int key, int value);
 }
 extern "C" int rr_set_tuning(int key, int value) {
-    if (key < 0 || key > 8) return fail(RR_EINVAL, "rr_set_tuning: unknown key");
+    if (key < 0 || key > 9) return fail(RR_EINVAL, "rr_set_tuning: unknown key");
+    if (key == RR_TUNE_KNN_FUSED) {
+        rr::g_knn_fused = value != 0;
+        return RR_OK;
+    }
     if (key == RR_TUNE_GRID_CUS) {
         if (value < 0) return fail(RR_EINVAL, "rr_set_tuning: RR_TUNE_GRID_CUS must be >= 0");
         rr::g_grid_cap = value;

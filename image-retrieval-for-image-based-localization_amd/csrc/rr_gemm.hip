@@ -393,6 +393,12 @@ __global__ void __launch_bounds__(64 * WC * WP, ((NS == 2 && AK * TC <= 256) || 
                     const long long o = (long long)p * a.ldy + c;
 #pragma unroll
                     for (int r = 0; r < 4; ++r) v[r] = v[r] * sc[r] + sh[r];
+                    if constexpr (sizeof(TO) == 4) {
+                        if (a.scr_k) {  // kNN screen: append survivors, store nothing
+                            screen_append(a, v, c, a.cout, p, a.scr_tau[p]);
+                            continue;
+                        }
+                    }
                     if (full) {
                         if (resid) {
                             float rv[4];
@@ -865,6 +871,12 @@ __global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int n
                         float v[4];
 #pragma unroll
                         for (int r = 0; r < 4; ++r) v[r] = acc[qa][qb][i][j][r] * sc[r] + sh[r];
+                        if constexpr (sizeof(TO) == 4) {
+                            if (a.scr_k) {  // kNN screen: append survivors, store nothing
+                                screen_append(a, v, c, a.cout, p, a.scr_tau[p]);
+                                continue;
+                            }
+                        }
                         const long long o = (long long)p * a.ldy + c;
                         if (full) {
                             if (resid) {

@@ -113,7 +113,42 @@ struct ConvArgs {
     float slope;
     int lc;  // log2(cin)
     int P;   // n*ho*wo
+    // kNN screening epilogue of the score GEMM (rr_knn.hip), float output only:
+    // when scr_k != nullptr nothing is stored to y; every score whose key is
+    // >= scr_tau[query] is appended to the (query, chunk) candidate slot
+    // (chunk = (scr_row0 + row) / scr_L, KC entries, scr_cnt counts appends).
+    uint32_t* scr_tau;
+    int* scr_cnt;
+    uint32_t* scr_k;
+    int* scr_i;
+    int scr_L, scr_nchunks, scr_KC, scr_row0;
 };
+
+// monotone uint32 key of a float score (larger score <-> larger key; 0 = sentinel)
+__device__ __forceinline__ uint32_t score_key(float f) {
+    const uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// Screening epilogue: 4 consecutive database rows c..c+3 (valid: < rows) of query p.
+__device__ __forceinline__ void screen_append(const ConvArgs& a, const float* v, int c, int rows, int p,
+                                              uint32_t tau) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        if (c + r >= rows) break;
+        const uint32_t key = score_key(v[r]);
+        if (key >= tau) {
+            const int grow = a.scr_row0 + c + r;
+            const int chunk = grow / a.scr_L;
+            const long long slot = (long long)p * a.scr_nchunks + chunk;
+            const int pos = atomicAdd(a.scr_cnt + slot, 1);
+            if (pos < a.scr_KC) {
+                a.scr_k[slot * a.scr_KC + pos] = key;
+                a.scr_i[slot * a.scr_KC + pos] = grow;
+            }
+        }
+    }
+}
 // scores[p][c] (f32, row stride ldy) = x[p][:] . w[c][:], 1x1 GEMM, dtype in.
 void gemm_scores(const ConvArgs& a, int dtype, hipStream_t s);
 

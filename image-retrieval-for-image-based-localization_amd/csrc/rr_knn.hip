@@ -40,6 +40,8 @@ static size_t slab_budget() {
     return b;
 }
 constexpr int MAX_SORT = 8192;
+constexpr int PREFIX_CHUNKS = 4;         // chunks through the slab path before the screening GEMM
+int g_knn_fused = 1;                     // rr_set_tuning(RR_TUNE_KNN_FUSED)
 constexpr int TOPK_BINS = 2048;          // radix-select histogram (11-bit digits)
 
 __device__ __forceinline__ uint32_t fkey(float f) {
@@ -50,76 +52,117 @@ __device__ __forceinline__ float funkey(uint32_t k) {
     return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
 }
 
-// Top-K (largest keys) of keys[0..len) with index-order ties.  `getk(i)` gives
-// the key, `geti(i)` the payload index; K results are written to out_k/out_i
-// in ascending position order; missing slots get (key 0, index -1).
-// SKIP0: key 0 marks a slot screened out before the select (below the query's
-// running threshold); such keys are neither counted nor emitted, `nvalid` is
-// the number of non-zero keys, and fewer than K of them are emitted in index
-// order followed by (0, -1) padding.  Returns the K-th key (0 when every valid
-// key was taken).
-template <bool SKIP0 = false, typename GK, typename GI>
+// Radix select of the K-th largest key of keys[0..len) (SKIP0: key 0 marks
+// a slot screened out before the select — neither counted nor emitted).
+// Returns the K-th key and sets *rem to how many keys equal to it belong to
+// the top K.  Precondition: more than K counted keys.
+template <bool SKIP0, typename GK>
+__device__ uint32_t radix_kth(GK getk, int len, int K, int* smem_i, int* rem) {
+    int* hist = smem_i;                        // TOPK_BINS
+    int* sel = smem_i + TOPK_BINS + 32;        // [0]=digit, [1]=remaining
+    const int tid = threadIdx.x;
+    int remaining = K;
+    // digits of 11, 11 and 10 bits: the first covers sign, exponent and two
+    // mantissa bits, so the scores' few exponents spread over many bins
+    // (fewer same-address LDS atomics than an 8-bit top digit), 3 passes.
+    uint32_t prefix = 0, mask = 0;
+    for (int pass = 0; pass < 3; ++pass) {
+        const int shift = pass == 0 ? 21 : pass == 1 ? 10 : 0;
+        const int bits = pass == 2 ? 10 : 11;
+        const uint32_t dmask = (1u << bits) - 1;
+        for (int i = tid; i < TOPK_BINS; i += SEL_THREADS) hist[i] = 0;
+        __syncthreads();
+        for (int i = tid; i < len; i += SEL_THREADS) {
+            uint32_t k = getk(i);
+            if ((k & mask) == prefix && (!SKIP0 || k != 0u)) atomicAdd(&hist[(k >> shift) & dmask], 1);
+        }
+        __syncthreads();
+        if (tid < 64) {
+            // wave 0: lane owns bins [32*tid, 32*tid + 32); suffix sums
+            // across lanes (lane 63 holds the highest digits), then a walk
+            // down its own bins to the digit holding the K-th key
+            constexpr int PER = TOPK_BINS / 64;
+            int lsum = 0;
+#pragma unroll
+            for (int e = 0; e < PER; ++e) lsum += hist[tid * PER + ((e + tid) & (PER - 1))];  // rotated: conflict-free
+            int sfx = lsum;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                int y = __shfl_down(sfx, o, 64);
+                if (tid + o < 64) sfx += y;
+            }
+            int acc = sfx - lsum;  // count of keys with digit above this lane's bins
+            if (acc < remaining && acc + lsum >= remaining) {
+                for (int e = PER - 1; e >= 0; --e) {
+                    const int c = hist[tid * PER + e];
+                    if (acc + c >= remaining) {
+                        sel[0] = tid * PER + e;
+                        sel[1] = remaining - acc;
+                        break;
+                    }
+                    acc += c;
+                }
+            }
+        }
+        __syncthreads();
+        const int digit = sel[0];
+        remaining = sel[1];
+        prefix |= (uint32_t)digit << shift;
+        mask |= dmask << shift;
+        __syncthreads();
+    }
+    *rem = remaining;
+    return prefix;
+}
+
+// Top-K (largest keys) of keys[0..len).  `getk(i)` gives the key, `geti(i)`
+// the payload index; K results are written to out_k/out_i in ascending
+// position order; missing slots get (key 0, index -1).
+// Ties at the K-th key: by position (IDXTIE false — the position order is the
+// index order for the chunk selects, whose keys come in row order) or by
+// smallest index (IDXTIE true — candidate pools appended by the screening
+// epilogue in arbitrary order; a second radix pass on ~index picks the
+// lowest indices among the tied keys).
+// SKIP0: key 0 marks a slot screened out before the select (below the
+// query's running threshold); such keys are neither counted nor emitted,
+// `nvalid` is the number of non-zero keys, and fewer than K of them are
+// emitted followed by (0, -1) padding.  Returns the K-th key (0 when every
+// valid key was taken).
+template <bool SKIP0 = false, bool IDXTIE = false, typename GK, typename GI>
 __device__ uint32_t block_topk(GK getk, GI geti, int len, int K, uint32_t* out_k, int* out_i, int* smem_i,
                                int nvalid = -1) {
     if (!SKIP0) nvalid = len;
-    int* hist = smem_i;                        // TOPK_BINS
     int* wsum = smem_i + TOPK_BINS;            // SEL_WAVES + 1
-    int* sel = smem_i + TOPK_BINS + 32;        // [0]=digit, [1]=remaining
     const int tid = threadIdx.x;
     uint32_t thr = 0;
     int remaining = K;
-    if (nvalid > K) {
-        // digits of 11, 11 and 10 bits: the first covers sign, exponent and two
-        // mantissa bits, so the scores' few exponents spread over many bins
-        // (fewer same-address LDS atomics than an 8-bit top digit), 3 passes.
-        uint32_t prefix = 0, mask = 0;
-        for (int pass = 0; pass < 3; ++pass) {
-            const int shift = pass == 0 ? 21 : pass == 1 ? 10 : 0;
-            const int bits = pass == 2 ? 10 : 11;
-            const uint32_t dmask = (1u << bits) - 1;
-            for (int i = tid; i < TOPK_BINS; i += SEL_THREADS) hist[i] = 0;
+    if (nvalid > K) thr = radix_kth<SKIP0>(getk, len, K, smem_i, &remaining);
+    // index tie-break: among the keys equal to thr, take the `remaining` smallest indices
+    bool itie = false;
+    int ithr = 0;
+    if constexpr (IDXTIE) {
+        if (nvalid > K && thr != 0u) {
+            int* cnt = smem_i + TOPK_BINS + 56;
+            if (tid == 0) cnt[0] = 0;
             __syncthreads();
-            for (int i = tid; i < len; i += SEL_THREADS) {
-                uint32_t k = getk(i);
-                if ((k & mask) == prefix && (!SKIP0 || k != 0u)) atomicAdd(&hist[(k >> shift) & dmask], 1);
-            }
-            __syncthreads();
-            if (tid < 64) {
-                // wave 0: lane owns bins [32*tid, 32*tid + 32); suffix sums
-                // across lanes (lane 63 holds the highest digits), then a walk
-                // down its own bins to the digit holding the K-th key
-                constexpr int PER = TOPK_BINS / 64;
-                int lsum = 0;
+            int e = 0;
+            for (int i = tid; i < len; i += SEL_THREADS) e += getk(i) == thr;
 #pragma unroll
-                for (int e = 0; e < PER; ++e) lsum += hist[tid * PER + ((e + tid) & (PER - 1))];  // rotated: conflict-free
-                int sfx = lsum;
-#pragma unroll
-                for (int o = 1; o < 64; o <<= 1) {
-                    int y = __shfl_down(sfx, o, 64);
-                    if (tid + o < 64) sfx += y;
-                }
-                int acc = sfx - lsum;  // count of keys with digit above this lane's bins
-                if (acc < remaining && acc + lsum >= remaining) {
-                    for (int e = PER - 1; e >= 0; --e) {
-                        const int c = hist[tid * PER + e];
-                        if (acc + c >= remaining) {
-                            sel[0] = tid * PER + e;
-                            sel[1] = remaining - acc;
-                            break;
-                        }
-                        acc += c;
-                    }
-                }
+            for (int o = 32; o > 0; o >>= 1) e += __shfl_xor(e, o, 64);
+            if ((tid & 63) == 0 && e) atomicAdd(cnt, e);
+            __syncthreads();
+            const int E = cnt[0];
+            __syncthreads();
+            if (E > remaining) {
+                int rem2;
+                const uint32_t t2 = radix_kth<true>(
+                    [&](int i) { return getk(i) == thr ? ~(uint32_t)geti(i) : 0u; }, len, remaining, smem_i, &rem2);
+                itie = true;
+                ithr = (int)~t2;  // indices are unique: exactly `remaining` tied keys have index <= ithr
             }
-            __syncthreads();
-            const int digit = sel[0];
-            remaining = sel[1];
-            prefix |= (uint32_t)digit << shift;
-            mask |= dmask << shift;
-            __syncthreads();
         }
-        thr = prefix;
     }
+    const int take_eq = itie ? 0x7fffffff : remaining;
     // ordered emission: wave w owns the contiguous range [wb, we) and walks it
     // 64 keys at a time (stride-1 reads); ballot + mbcnt give each key's rank
     // among the taken keys before it, one 16-entry scan orders the waves.
@@ -129,13 +172,16 @@ __device__ uint32_t block_topk(GK getk, GI geti, int len, int K, uint32_t* out_k
     const bool sel_all = nvalid <= K;
     const int wseg = (((len + SEL_WAVES - 1) / SEL_WAVES) + 63) & ~63;
     const int wb = min(len, w * wseg), we = min(len, wb + wseg);
+    auto is_eq = [&](bool in, uint32_t k, int i) {
+        return in && !sel_all && k == thr && (!itie || geti(i) <= ithr);
+    };
     int cgt = 0, ceq = 0;
     for (int i0 = wb; i0 < we; i0 += 64) {
         const int i = i0 + lane;
         const bool in = i < we;
         const uint32_t k = in ? getk(i) : 0u;
         cgt += __popcll(__ballot(in && (sel_all ? (!SKIP0 || k != 0u) : k > thr)));
-        ceq += __popcll(__ballot(in && !sel_all && k == thr));
+        ceq += __popcll(__ballot(is_eq(in, k, i)));
     }
     if (lane == 0) {
         wgt[w] = cgt;
@@ -152,15 +198,15 @@ __device__ uint32_t block_topk(GK getk, GI geti, int len, int K, uint32_t* out_k
         const bool in = i < we;
         const uint32_t k = in ? getk(i) : 0u;
         const bool gt = in && (sel_all ? (!SKIP0 || k != 0u) : k > thr);
-        const bool eq = in && !sel_all && k == thr;
+        const bool eq = is_eq(in, k, i);
         const unsigned long long bg = __ballot(gt), be = __ballot(eq);
         const int rg = pgt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bg >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bg, 0u));
         const int re = peq + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(be >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)be, 0u));
         if (gt) {
-            const int slot = rg + min(re, remaining);
+            const int slot = rg + min(re, take_eq);
             out_k[slot] = k;
             out_i[slot] = geti(i);
-        } else if (eq && re < remaining) {
+        } else if (eq && re < take_eq) {
             out_k[rg + re] = k;
             out_i[rg + re] = geti(i);
         }
@@ -297,11 +343,6 @@ __global__ void __launch_bounds__(SEL_THREADS) k_chunk_select(const float* __res
     if (threadIdx.x == 0 && nvalid > KC && thr > tq) atomicMax(tau + q, thr);
 }
 
-__global__ void k_zero_u32(uint32_t* p, int n) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) p[i] = 0u;
-}
-
 // ------------------------------------------------------------------ bitonic
 // Struct-of-arrays sort of (score f64, index) pairs, best first:
 // better(a, b) = a.s > b.s || (a.s == b.s && a.i < b.i).  Sentinel: (-inf, MAX).
@@ -336,15 +377,69 @@ __device__ void bitonic_best_first(double* ks, I* is, int n) {
 //  k_rescore       grid (npow2/4, nq): one wave per candidate, float64 score
 //  k_final_sort    grid (nq):          bitonic (score desc, index asc), emit k
 __global__ void __launch_bounds__(SEL_THREADS) k_final_select(const uint32_t* __restrict__ cand_k,
-                                                              const int* __restrict__ cand_i, int ncand, int KC,
+                                                              const int* __restrict__ cand_i,
+                                                              const int* __restrict__ cnt, int nchunks, int KC,
                                                               uint32_t* __restrict__ sel_k, int* __restrict__ sel_i) {
     __shared__ int smi[TOPK_BINS + 64];
     const int q = blockIdx.x;
+    const int ncand = nchunks * KC;
     const uint32_t* ck = cand_k + (long long)q * ncand;
     const int* ci = cand_i + (long long)q * ncand;
-    // sentinel candidates (index -1) carry key 0 = below every real score key
-    block_topk([&](int i) { return ck[i]; }, [&](int i) { return ci[i]; }, ncand, KC, sel_k + (long long)q * KC,
-               sel_i + (long long)q * KC, smi);
+    const int* cq = cnt + (long long)q * nchunks;
+    // slot (chunk c, position j) holds a candidate when j < min(cnt, KC); the
+    // chunk selects fill whole slots (sentinels (0, -1) past their survivors),
+    // the screening epilogue appends in arbitrary order -> ties by index
+    auto valid = [&](int i) { const int c = i / KC; return i - c * KC < min(cq[c], KC); };
+    block_topk<false, true>([&](int i) { return valid(i) ? ck[i] : 0u; }, [&](int i) { return valid(i) ? ci[i] : -1; },
+                            ncand, KC, sel_k + (long long)q * KC, sel_i + (long long)q * KC, smi);
+}
+
+// tau[q] = 0 and the slot counts: chunks [0, g0) are filled whole by the
+// chunk select (count KC), the others start empty (screening epilogue).
+__global__ void k_knn_reset(uint32_t* __restrict__ tau, int* __restrict__ cnt, int nq, int nchunks, int g0, int KC,
+                            int zero_tau) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (zero_tau && i < nq) tau[i] = 0u;
+    if (i < (long long)nq * nchunks) cnt[i] = (int)(i % nchunks) < g0 ? KC : 0;
+}
+
+// Overflow fix-up of the screened chunks: a (query, chunk) slot that received
+// more than KC survivors (the prefix threshold was too low for that chunk —
+// e.g. many near-duplicates of the query there) is rebuilt exactly: the
+// chunk's scores for that query are recomputed (one wave per row, f32
+// accumulation of the screening-dtype rows) and radix-selected in row order,
+// like the chunk select.  One block per query walks its chunks; chunks that
+// did not overflow cost one load.
+template <typename T>
+__global__ void __launch_bounds__(SEL_THREADS) k_slot_fixup(const T* __restrict__ db, long long n_db, const T* __restrict__ q,
+                                                            int d, int L, int nchunks, int g0, int KC,
+                                                            int* __restrict__ cnt, uint32_t* __restrict__ cand_k,
+                                                            int* __restrict__ cand_i, uint32_t* __restrict__ tau) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t keys[];  // L
+    __shared__ int smi[TOPK_BINS + 64];
+    const int qi = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const T* qr = q + (long long)qi * d;
+    for (int c = g0; c < nchunks; ++c) {
+        const long long slot = (long long)qi * nchunks + c;
+        if (cnt[slot] <= KC) continue;  // block-uniform
+        const long long r0 = (long long)c * L;
+        const int len = (int)min((long long)L, n_db - r0);
+        for (int r = w; r < len; r += SEL_WAVES) {
+            const T* dr = db + (r0 + r) * d;
+            float acc = 0.f;
+            for (int t = lane; t < d; t += 64) acc += DT<T>::to_f(dr[t]) * DT<T>::to_f(qr[t]);
+            acc = wave_sum(acc);
+            if (lane == 0) keys[r] = score_key(acc);
+        }
+        __syncthreads();
+        const uint32_t thr = block_topk([&](int i) { return keys[i]; }, [&](int i) { return (int)(r0 + i); }, len, KC,
+                                        cand_k + slot * KC, cand_i + slot * KC, smi);
+        if (threadIdx.x == 0) {
+            cnt[slot] = KC;
+            if (len > KC && thr > tau[qi]) atomicMax(tau + qi, thr);
+        }
+        __syncthreads();
+    }
 }
 
 // float64 re-score from the float32 rows: exact products, a fixed per-lane
@@ -441,7 +536,7 @@ static int pow2_at_least(int v) {
 struct KnnPlan {
     int L, nchunks, G, KC, npow2;
     long long S;
-    size_t slab_bytes, cand_bytes, sel_bytes, fin_bytes, tau_bytes, total;
+    size_t slab_bytes, cand_bytes, sel_bytes, fin_bytes, tau_bytes, cnt_bytes, total;
 };
 
 static int default_cand(int k, int dtype) {
@@ -467,7 +562,9 @@ static KnnPlan plan(long long n_db, int nq, int k, int cand, int dtype) {
     p.sel_bytes = ((size_t)nq * p.KC * 4 + 255) / 256 * 256;
     p.fin_bytes = ((size_t)nq * p.npow2 * 8 + 255) / 256 * 256 + ((size_t)nq * p.npow2 * 4 + 255) / 256 * 256;
     p.tau_bytes = ((size_t)nq * 4 + 255) / 256 * 256;
-    p.total = p.slab_bytes + 2 * ((p.cand_bytes + 255) / 256 * 256) + 2 * p.sel_bytes + p.fin_bytes + p.tau_bytes;
+    p.cnt_bytes = ((size_t)nq * p.nchunks * 4 + 255) / 256 * 256;
+    p.total = p.slab_bytes + 2 * ((p.cand_bytes + 255) / 256 * 256) + 2 * p.sel_bytes + p.fin_bytes + p.tau_bytes +
+              p.cnt_bytes;
     return p;
 }
 
@@ -506,23 +603,38 @@ int rr_knn_topk(const void* db, const float* db_f32, long long n_db, const void*
     double* fin_s = (double*)(fws + 2 * p.sel_bytes);
     int* fin_i = (int*)(fws + 2 * p.sel_bytes + ((size_t)nq * p.npow2 * 8 + 255) / 256 * 256);
     uint32_t* tau = (uint32_t*)(fws + 2 * p.sel_bytes + p.fin_bytes);
+    int* cnt = (int*)(fws + 2 * p.sel_bytes + p.fin_bytes + p.tau_bytes);
 
     static bool attr_done = false;
     if (!attr_done) {
         (void)hipFuncSetAttribute((const void*)k_chunk_select, hipFuncAttributeMaxDynamicSharedMemorySize, CHUNK_L * 4);
+        (void)hipFuncSetAttribute((const void*)k_slot_fixup<bf16_t>, hipFuncAttributeMaxDynamicSharedMemorySize, CHUNK_L * 4);
+        (void)hipFuncSetAttribute((const void*)k_slot_fixup<f16_t>, hipFuncAttributeMaxDynamicSharedMemorySize, CHUNK_L * 4);
+        (void)hipFuncSetAttribute((const void*)k_slot_fixup<float>, hipFuncAttributeMaxDynamicSharedMemorySize, CHUNK_L * 4);
         (void)hipFuncSetAttribute((const void*)k_final_sort, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 4096);
         (void)hipFuncSetAttribute((const void*)k_merge, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 4096);
         attr_done = true;
     }
 
     const size_t esz = dtype == RR_F32 ? 4 : 2;
+    // Screening (default): the first PREFIX_CHUNKS chunks go through the score
+    // slab + chunk select, which sets each query's running threshold tau; the
+    // rest of the database is ONE score GEMM whose epilogue appends only the
+    // scores >= tau to per-(query, chunk) slots (no slab write / read, no
+    // select launch); overflowing slots are rebuilt by k_slot_fixup.
+    // RR_KNN_FUSED=0: every chunk through the slab (the round-1 pipeline).
+    static const int fused_env = getenv("RR_KNN_FUSED") && getenv("RR_KNN_FUSED")[0] == '0' ? 0 : 1;
+    const bool fused = fused_env && g_knn_fused && p.nchunks > PREFIX_CHUNKS && (d * esz) % 128 == 0;
+    const int g0 = fused ? PREFIX_CHUNKS : p.nchunks;
+    const long long slab_rows = (long long)g0 * p.L < n_db ? (long long)g0 * p.L : n_db;
     // the running threshold is reset by a kernel (RR_KNN_TAU_MEMSET=1: by
     // hipMemsetAsync, kept to reproduce the graph-replay finding of DESIGN §4)
     static const bool tau_memset = getenv("RR_KNN_TAU_MEMSET") && getenv("RR_KNN_TAU_MEMSET")[0] == '1';
     if (tau_memset) (void)hipMemsetAsync(tau, 0, (size_t)nq * 4, s);
-    else hipLaunchKernelGGL(k_zero_u32, dim3((nq + 255) / 256), dim3(256), 0, s, tau, nq);
-    for (long long r0 = 0; r0 < n_db; r0 += (long long)p.G * p.L) {
-        const int rows = (int)((n_db - r0) < (long long)p.G * p.L ? (n_db - r0) : (long long)p.G * p.L);
+    const long long nreset = (long long)nq * p.nchunks > nq ? (long long)nq * p.nchunks : nq;
+    hipLaunchKernelGGL(k_knn_reset, dim3((unsigned)((nreset + 255) / 256)), dim3(256), 0, s, tau, cnt, nq, p.nchunks, g0,
+                       p.KC, tau_memset ? 0 : 1);
+    auto score_args = [&](long long r0, int rows) {
         ConvArgs a{};
         a.x = q;
         a.w = (const char*)db + (size_t)r0 * d * esz;
@@ -532,14 +644,35 @@ int rr_knn_topk(const void* db, const float* db_f32, long long n_db, const void*
         a.act = RR_ACT_IDENTITY; a.flags = 0; a.slope = 0.f;
         a.lc = __builtin_ctz((unsigned)d);
         a.P = nq;
-        gemm_scores(a, dtype, s);
+        return a;
+    };
+    for (long long r0 = 0; r0 < slab_rows; r0 += (long long)p.G * p.L) {
+        const int rows = (int)((slab_rows - r0) < (long long)p.G * p.L ? (slab_rows - r0) : (long long)p.G * p.L);
+        gemm_scores(score_args(r0, rows), dtype, s);
         const int chunks = (rows + p.L - 1) / p.L;
         hipLaunchKernelGGL(k_chunk_select, dim3(nq, chunks), dim3(SEL_THREADS), (size_t)p.L * 4, s, slab, p.S, p.L,
                            rows, (int)r0, (int)(r0 / p.L), p.nchunks, p.KC, cand_k, cand_i, tau);
     }
+    if (fused) {
+        ConvArgs a = score_args(slab_rows, (int)(n_db - slab_rows));
+        a.scr_tau = tau; a.scr_cnt = cnt; a.scr_k = cand_k; a.scr_i = cand_i;
+        a.scr_L = p.L; a.scr_nchunks = p.nchunks; a.scr_KC = p.KC; a.scr_row0 = (int)slab_rows;
+        gemm_scores(a, dtype, s);
+        const dim3 g(nq), b(SEL_THREADS);
+        const size_t lds = (size_t)p.L * 4;
+        if (dtype == RR_BF16)
+            hipLaunchKernelGGL(k_slot_fixup<bf16_t>, g, b, lds, s, (const bf16_t*)db, n_db, (const bf16_t*)q, d, p.L,
+                               p.nchunks, g0, p.KC, cnt, cand_k, cand_i, tau);
+        else if (dtype == RR_F16)
+            hipLaunchKernelGGL(k_slot_fixup<f16_t>, g, b, lds, s, (const f16_t*)db, n_db, (const f16_t*)q, d, p.L,
+                               p.nchunks, g0, p.KC, cnt, cand_k, cand_i, tau);
+        else
+            hipLaunchKernelGGL(k_slot_fixup<float>, g, b, lds, s, (const float*)db, n_db, (const float*)q, d, p.L,
+                               p.nchunks, g0, p.KC, cnt, cand_k, cand_i, tau);
+    }
     const size_t fin_lds = (size_t)p.npow2 * 12;
     if (fin_lds > 160 * 1024 - 4096) return fail(RR_EINVAL, "rr_knn_topk: candidate set exceeds LDS");
-    hipLaunchKernelGGL(k_final_select, dim3(nq), dim3(SEL_THREADS), 0, s, cand_k, cand_i, p.nchunks * p.KC, p.KC,
+    hipLaunchKernelGGL(k_final_select, dim3(nq), dim3(SEL_THREADS), 0, s, cand_k, cand_i, cnt, p.nchunks, p.KC,
                        sel_k, sel_i);
     hipLaunchKernelGGL(k_rescore, dim3((p.npow2 + 3) / 4, nq), dim3(256), 0, s, sel_i, p.KC, p.npow2, db_f32, q_f32, d,
                        fin_s, fin_i);

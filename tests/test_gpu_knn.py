@@ -184,3 +184,68 @@ def test_knn_full_size_1m_bench_shape(cuda):
         ii.append(sh_i)
     sm, im = merge_topk(torch.stack(ss), torch.stack(ii), k)
     assert torch.equal(im, i) and torch.equal(sm, s)
+
+
+def _fused_vs_slab(cuda, db, qq, k, prec):
+    """search with the screening-epilogue pipeline (default) and with every chunk
+    through the score slab (RR_TUNE_KNN_FUSED = 0)"""
+    from cirtorch import _engine as E
+    from cirtorch.search import KnnIndex
+    index = KnnIndex(torch.from_numpy(db).to(cuda), prec)
+    q = torch.from_numpy(qq).to(cuda)
+    s1, i1 = index.search(q, k)
+    E.check(E.lib().rr_set_tuning(9, 0), "rr_set_tuning")
+    try:
+        s0, i0 = index.search(q, k)
+    finally:
+        E.lib().rr_set_tuning(9, 1)
+    return (s1.cpu().numpy(), i1.cpu().numpy()), (s0.cpu().numpy(), i0.cpu().numpy())
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16", "fp32"])
+def test_knn_fused_screen_stress(cuda, prec):
+    """Databases past the 4-chunk prefix (65536 rows), so the screening GEMM
+    epilogue runs: (a) scores rising row after row — every screened chunk
+    overflows its slot and is rebuilt by the fix-up kernel; (b) blocks of the
+    prefix duplicated in screened chunks — equal keys across the two paths,
+    the lower index must win; (c) all rows equal — every key ties; (d) 600
+    near-copies of one query planted in one chunk — a single overflowing slot.
+    Results equal the exact oracle and the all-slab pipeline."""
+    from oracle import data, ops
+    d = 128
+    base = data.unit_rows(40000, d, seed=61)
+    qq = data.unit_rows(4, d, seed=62)
+    t = np.linspace(0.0, 1.0, 180000, dtype=np.float32)[:, None]
+    rise = qq[:1] * t + data.unit_rows(180000, d, seed=63)
+    rise = (rise / np.linalg.norm(rise, axis=1, keepdims=True)).astype(np.float32)
+    dup = np.concatenate([base, base, base, base[:30000]], 0)                     # 150k rows
+    same = np.repeat(base[:1], 100000, 0)
+    plant = data.unit_rows(170000, d, seed=64)
+    plant[140000:140600] = qq[2] + 0.01 * data.unit_rows(600, d, seed=65)
+    plant[140000:140600] /= np.linalg.norm(plant[140000:140600], axis=1, keepdims=True)
+    for name, db in (("rise", rise), ("dup", dup), ("same", same), ("plant", plant)):
+        ref_s, ref_i = ops.topk_exact(db, qq, 100)
+        (s1, i1), (s0, i0) = _fused_vs_slab(cuda, db, qq, 100, prec)
+        np.testing.assert_array_equal(i1, ref_i, err_msg="%s %s fused" % (name, prec))
+        np.testing.assert_array_equal(i0, ref_i, err_msg="%s %s slab" % (name, prec))
+        np.testing.assert_allclose(s1, ref_s, rtol=0, atol=1e-12)
+        assert np.array_equal(s1, s0)
+
+
+def test_knn_fused_graph_replay(cuda):
+    """The screening pipeline (reset, prefix, fused GEMM, fix-up) captured in a
+    hipGraph and replayed equals eager launches."""
+    from cirtorch.search import KnnIndex
+    from cirtorch.utils.graph import GraphedForward
+    from oracle import data, ops
+    db = torch.from_numpy(data.unit_rows(120000, 256, seed=71)).to(cuda)
+    q1 = torch.from_numpy(data.unit_rows(300, 256, seed=72)).to(cuda)
+    q2 = torch.from_numpy(data.unit_rows(300, 256, seed=73)).to(cuda)
+    index = KnnIndex(db, "bf16")
+    g = GraphedForward(lambda q: index.search(q, 50), q1)
+    for q in (q1, q2, q1):
+        s, i = g(q)
+        es, ei = index.search(q, 50)
+        assert torch.equal(i, ei) and torch.equal(s, es)
+    ref_s, ref_i = ops.topk_exact(db.cpu().numpy(), q2.cpu().numpy(), 50)
+    np.testing.assert_array_equal(index.search(q2, 50)[1].cpu().numpy(), ref_i)
