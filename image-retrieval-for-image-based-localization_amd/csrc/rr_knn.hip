@@ -39,6 +39,7 @@ static size_t slab_budget() {
     }
     return b;
 }
+typedef __attribute__((ext_vector_type(4))) float f32x4_knn_t;
 constexpr int MAX_SORT = 8192;
 constexpr int PREFIX_CHUNKS = 4;         // chunks through the slab path before the screening GEMM
 int g_knn_fused = 1;                     // rr_set_tuning(RR_TUNE_KNN_FUSED)
@@ -406,10 +407,44 @@ __global__ void k_knn_reset(uint32_t* __restrict__ tau, int* __restrict__ cnt, i
 // Overflow fix-up of the screened chunks: a (query, chunk) slot that received
 // more than KC survivors (the prefix threshold was too low for that chunk —
 // e.g. many near-duplicates of the query there) is rebuilt exactly: the
-// chunk's scores for that query are recomputed (one wave per row, f32
-// accumulation of the screening-dtype rows) and radix-selected in row order,
-// like the chunk select.  One block per query walks its chunks; chunks that
-// did not overflow cost one load.
+// chunk's scores for that query are recomputed and radix-selected in row
+// order, like the chunk select.  The scores must be the SAME bits the score
+// GEMM produced (ties across chunks are broken by index only when equal rows
+// get equal keys), so they are recomputed with the GEMM's own MFMA, operand
+// layout and K order: 16 rows per MFMA as the A operand, the query as column
+// 0 of B (the other columns zero; every output element is an independent dot
+// product of its row and column).  One block per query walks its chunks;
+// chunks that did not overflow cost one load.
+template <typename T>
+__device__ __forceinline__ void fixup_scores(const T* __restrict__ dr, bool row_ok, const T* __restrict__ qr, bool col0,
+                                             int d, f32x4_knn_t& acc) {
+    const int kq = (threadIdx.x & 63) >> 4;
+    if constexpr (sizeof(T) == 2) {
+        for (int k0 = 0; k0 < d; k0 += 64) {
+#pragma unroll
+            for (int hs = 0; hs < 2; ++hs) {
+                const int off = k0 + (kq + 4 * hs) * 8;
+                const uint4 av = row_ok ? *reinterpret_cast<const uint4*>(dr + off) : make_uint4(0, 0, 0, 0);
+                const uint4 bv = col0 ? *reinterpret_cast<const uint4*>(qr + off) : make_uint4(0, 0, 0, 0);
+                acc = H16<T>::mfma(av, bv, acc);
+            }
+        }
+    } else {
+        for (int k0 = 0; k0 < d; k0 += 32) {
+#pragma unroll
+            for (int hs = 0; hs < 2; ++hs) {
+                const int off = k0 + (kq + 4 * hs) * 4;
+                const float4 av = row_ok ? *reinterpret_cast<const float4*>(dr + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+                const float4 bv = col0 ? *reinterpret_cast<const float4*>(qr + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, acc, 0, 0, 0);
+            }
+        }
+    }
+}
+
 template <typename T>
 __global__ void __launch_bounds__(SEL_THREADS) k_slot_fixup(const T* __restrict__ db, long long n_db, const T* __restrict__ q,
                                                             int d, int L, int nchunks, int g0, int KC,
@@ -418,18 +453,22 @@ __global__ void __launch_bounds__(SEL_THREADS) k_slot_fixup(const T* __restrict_
     extern __shared__ __attribute__((aligned(16))) uint32_t keys[];  // L
     __shared__ int smi[TOPK_BINS + 64];
     const int qi = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r16 = lane & 15, kq = lane >> 4;
     const T* qr = q + (long long)qi * d;
     for (int c = g0; c < nchunks; ++c) {
         const long long slot = (long long)qi * nchunks + c;
         if (cnt[slot] <= KC) continue;  // block-uniform
         const long long r0 = (long long)c * L;
         const int len = (int)min((long long)L, n_db - r0);
-        for (int r = w; r < len; r += SEL_WAVES) {
-            const T* dr = db + (r0 + r) * d;
-            float acc = 0.f;
-            for (int t = lane; t < d; t += 64) acc += DT<T>::to_f(dr[t]) * DT<T>::to_f(qr[t]);
-            acc = wave_sum(acc);
-            if (lane == 0) keys[r] = score_key(acc);
+        for (int g = w * 16; g < len; g += SEL_WAVES * 16) {  // 16 rows per wave step
+            const bool row_ok = g + r16 < len;
+            f32x4_knn_t acc = (f32x4_knn_t){0.f, 0.f, 0.f, 0.f};
+            fixup_scores<T>(db + (r0 + g + (row_ok ? r16 : 0)) * d, row_ok, qr, r16 == 0, d, acc);
+            if (r16 == 0) {  // D[row 4 kq + e][column 0]
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (g + 4 * kq + e < len) keys[g + 4 * kq + e] = score_key(acc[e] * 1.f + 0.f);  // as the GEMM epilogue (-0 -> +0)
+            }
         }
         __syncthreads();
         const uint32_t thr = block_topk([&](int i) { return keys[i]; }, [&](int i) { return (int)(r0 + i); }, len, KC,
