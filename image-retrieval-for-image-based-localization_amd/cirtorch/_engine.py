@@ -59,6 +59,7 @@ _SIGS = {
     "rr_head_l2n_whiten_l2n": ([_vp, _i, _i, _vp, _vp, _i, _f, _vp, _vp, _vp], _i),
     "rr_knn_workspace_bytes": ([_ll, _i, _i, _i, _i, _i], _sz),
     "rr_knn_topk": ([_vp, _vp, _ll, _vp, _vp, _i, _i, _i, _i, _ll, _vp, _vp, _vp, _sz, _i, _vp], _i),
+    "rr_knn_topk_checked": ([_vp, _vp, _ll, _vp, _vp, _i, _i, _i, _i, _ll, _vp, _vp, _vp, _sz, _i, _f, _vp, _vp], _i),
     "rr_topk_merge": ([_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp], _i),
     "rr_local_head_workspace_bytes": ([_ll, _i, _i], _sz),
     "rr_local_head": ([_vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _vp, _i, _vp, _vp, _sz, _vp], _i),

@@ -278,10 +278,12 @@ def knn_workspace_bytes(n_db, nq, d, k, cand=0, dtype=torch.float32):
     return int(E.lib().rr_knn_workspace_bytes(int(n_db), int(nq), int(d), int(k), int(cand), E.dtype_code(dtype)))
 
 
-def knn_topk(db, db_f32, q, q_f32, k, cand=0, idx_offset=0, workspace=None):
+def knn_topk(db, db_f32, q, q_f32, k, cand=0, idx_offset=0, workspace=None, db_norm_max=None):
     """db/q: [n, D] rows in the screening dtype (float32, bfloat16 or float16);
     db_f32/q_f32: the float32 rows used for the exact re-score.
-    Returns (scores float64 [Q, k], idx int64 [Q, k])."""
+    Returns (scores float64 [Q, k], idx int64 [Q, k]); with db_norm_max (the
+    largest database row norm) also int32 [Q] flags: 1 where the screening
+    margin could not be certified (rr_knn_topk_checked)."""
     E.require_gpu(db, db_f32, q, q_f32)
     assert db.dtype == q.dtype and db_f32.dtype == torch.float32 and q_f32.dtype == torch.float32
     for t in (db, db_f32, q, q_f32):
@@ -293,10 +295,17 @@ def knn_topk(db, db_f32, q, q_f32, k, cand=0, idx_offset=0, workspace=None):
         workspace = torch.empty(need, dtype=torch.uint8, device=db.device)
     out_s = torch.empty((nq, k), dtype=torch.float64, device=db.device)
     out_i = torch.empty((nq, k), dtype=torch.int64, device=db.device)
-    E.check(E.lib().rr_knn_topk(E.ptr(db), E.ptr(db_f32), n_db, E.ptr(q), E.ptr(q_f32), nq, d, k, int(cand),
-                                int(idx_offset), E.ptr(out_s), E.ptr(out_i), E.ptr(workspace),
-                                workspace.numel(), E.dtype_code(db.dtype), _st()), "rr_knn_topk")
-    return out_s, out_i
+    if db_norm_max is None:
+        E.check(E.lib().rr_knn_topk(E.ptr(db), E.ptr(db_f32), n_db, E.ptr(q), E.ptr(q_f32), nq, d, k, int(cand),
+                                    int(idx_offset), E.ptr(out_s), E.ptr(out_i), E.ptr(workspace),
+                                    workspace.numel(), E.dtype_code(db.dtype), _st()), "rr_knn_topk")
+        return out_s, out_i
+    unc = torch.empty(nq, dtype=torch.int32, device=db.device)
+    E.check(E.lib().rr_knn_topk_checked(E.ptr(db), E.ptr(db_f32), n_db, E.ptr(q), E.ptr(q_f32), nq, d, k, int(cand),
+                                        int(idx_offset), E.ptr(out_s), E.ptr(out_i), E.ptr(workspace),
+                                        workspace.numel(), E.dtype_code(db.dtype), float(db_norm_max), E.ptr(unc),
+                                        _st()), "rr_knn_topk_checked")
+    return out_s, out_i, unc
 
 
 def topk_merge(scores, idx, k):

@@ -78,10 +78,25 @@ class KnnIndex:
             self._ws[stream.cuda_stream] = ws
         return ws
 
-    def search(self, q_rows, k):
+    def norm_max(self):
+        """largest database row norm (computed once; one device->host read)"""
+        if getattr(self, "_norm_max", None) is None:
+            self._norm_max = float(self.db32.norm(dim=1).max().item()) if self.ntotal else 0.0
+        return self._norm_max
+
+    def search(self, q_rows, k, verify=False):
         """q_rows [Q, D] -> (scores float64 [Q, k], idx int64 [Q, k]) on the current stream.
         An empty shard (ntotal == 0) returns k (-inf, -1) entries per query, which
-        the sharded merge drops."""
+        the sharded merge drops.
+
+        verify=True certifies the screening margin of every query (the rows left
+        out are provably below the returned k-th score given the screening
+        dtype's error bound) and re-searches uncertain queries — clusters of
+        near-duplicates tighter than the bf16 / fp16 screening error — with
+        float32 screening and more candidates; this costs one device->host
+        read per search (no graph capture)."""
+        if verify:
+            return self._search_verified(q_rows, k)
         if q_rows.shape[1] != self.dim:
             raise RuntimeError("KnnIndex.search: queries have D=%d, the database D=%d" % (q_rows.shape[1], self.dim))
         q32 = _pad_cols(q_rows.float().contiguous(), self.d_pad)
@@ -92,6 +107,32 @@ class KnnIndex:
         need = _ops.knn_workspace_bytes(self.ntotal, q.shape[0], q.shape[1], k, self.cand, self.dtype)
         return _ops.knn_topk(self.db, self.db32, q, q32, k, cand=self.cand, idx_offset=self.idx_offset,
                              workspace=self._workspace(need, q.device))
+
+
+    def _search_verified(self, q_rows, k):
+        if self.ntotal == 0 or q_rows.shape[0] == 0:
+            return self.search(q_rows, k)
+        q32 = _pad_cols(q_rows.float().contiguous(), self.d_pad)
+        q = _ops.cast_screen(q32, self.dtype)
+        need = _ops.knn_workspace_bytes(self.ntotal, q.shape[0], q.shape[1], k, self.cand, self.dtype)
+        s, i, unc = _ops.knn_topk(self.db, self.db32, q, q32, k, cand=self.cand, idx_offset=self.idx_offset,
+                                  workspace=self._workspace(need, q.device), db_norm_max=self.norm_max())
+        bad = torch.nonzero(unc).flatten()
+        if bad.numel() == 0:
+            return s, i
+        # re-search: float32 screening (error ~d 2^-24), then the largest candidate pool
+        for cand in (0, min(8192, max(1024, 8 * k))):
+            qb = q32[bad].contiguous()
+            need = _ops.knn_workspace_bytes(self.ntotal, qb.shape[0], qb.shape[1], k, cand, torch.float32)
+            s2, i2, u2 = _ops.knn_topk(self.db32, self.db32, qb, qb, k, cand=cand, idx_offset=self.idx_offset,
+                                       workspace=self._workspace(need, qb.device), db_norm_max=self.norm_max())
+            s[bad], i[bad] = s2, i2
+            keep = torch.nonzero(u2).flatten()
+            if keep.numel() == 0:
+                return s, i
+            bad = bad[keep]
+        raise RuntimeError("KnnIndex.search(verify=True): %d queries have more than 8192 near-tied candidates "
+                           "within the float32 screening error" % bad.numel())
 
 
 def knn(vecs, qvecs, k, precision="fp32", cand=0):

@@ -380,7 +380,8 @@ __device__ void bitonic_best_first(double* ks, I* is, int n) {
 __global__ void __launch_bounds__(SEL_THREADS) k_final_select(const uint32_t* __restrict__ cand_k,
                                                               const int* __restrict__ cand_i,
                                                               const int* __restrict__ cnt, int nchunks, int KC,
-                                                              uint32_t* __restrict__ sel_k, int* __restrict__ sel_i) {
+                                                              uint32_t* __restrict__ sel_k, int* __restrict__ sel_i,
+                                                              uint32_t* __restrict__ sel_thr) {
     __shared__ int smi[TOPK_BINS + 64];
     const int q = blockIdx.x;
     const int ncand = nchunks * KC;
@@ -391,8 +392,12 @@ __global__ void __launch_bounds__(SEL_THREADS) k_final_select(const uint32_t* __
     // chunk selects fill whole slots (sentinels (0, -1) past their survivors),
     // the screening epilogue appends in arbitrary order -> ties by index
     auto valid = [&](int i) { const int c = i / KC; return i - c * KC < min(cq[c], KC); };
-    block_topk<false, true>([&](int i) { return valid(i) ? ck[i] : 0u; }, [&](int i) { return valid(i) ? ci[i] : -1; },
-                            ncand, KC, sel_k + (long long)q * KC, sel_i + (long long)q * KC, smi);
+    const uint32_t thr = block_topk<false, true>([&](int i) { return valid(i) ? ck[i] : 0u; },
+                                                 [&](int i) { return valid(i) ? ci[i] : -1; }, ncand, KC,
+                                                 sel_k + (long long)q * KC, sel_i + (long long)q * KC, smi);
+    // every row outside the KC candidates has a screening key <= thr: a chunk's
+    // own KC-th key, the running threshold and the pool's KC-th key are all <= it
+    if (threadIdx.x == 0) sel_thr[q] = thr;
 }
 
 // tau[q] = 0 and the slot counts: chunks [0, g0) are filled whole by the
@@ -516,10 +521,18 @@ __global__ void __launch_bounds__(256) k_rescore(const int* __restrict__ sel_i, 
     }
 }
 
+// Certificate of the screening margin (out_unc != nullptr): every row left
+// out of the candidates has screening score <= funkey(thr) and hence exact
+// score <= funkey(thr) + delta, delta = delta_scale * ||q|| (the screening
+// error bound); if that is below the exact k-th score the top k are exact,
+// else the query is flagged (dense clusters tighter than the screening error).
 __global__ void __launch_bounds__(SEL_THREADS) k_final_sort(const double* __restrict__ fin_s,
                                                             const int* __restrict__ fin_i, int npow2, int k,
                                                             long long idx_offset, double* __restrict__ out_s,
-                                                            long long* __restrict__ out_i) {
+                                                            long long* __restrict__ out_i,
+                                                            const uint32_t* __restrict__ sel_thr,
+                                                            const float* __restrict__ q32, int d, double delta_scale,
+                                                            int* __restrict__ out_unc) {
     extern __shared__ __attribute__((aligned(16))) char dyn[];
     double* ks = reinterpret_cast<double*>(dyn);
     int* is = reinterpret_cast<int*>(ks + npow2);
@@ -534,6 +547,22 @@ __global__ void __launch_bounds__(SEL_THREADS) k_final_sort(const double* __rest
         const int i = is[j];
         out_s[(long long)q * k + j] = ks[j];
         out_i[(long long)q * k + j] = i == 0x7fffffff ? -1 : (long long)i + idx_offset;
+    }
+    if (out_unc) {
+        __shared__ double red[SEL_WAVES];
+        double ss = 0.0;
+        for (int t = threadIdx.x; t < d; t += SEL_THREADS) ss += (double)q32[(long long)q * d + t] * q32[(long long)q * d + t];
+        ss = wave_sum_d(ss);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double tot = 0.0;
+            for (int w = 0; w < SEL_WAVES; ++w) tot += red[w];
+            const uint32_t thr = sel_thr[q];
+            const bool full = k > npow2 || is[k - 1] == 0x7fffffff;  // fewer than k rows: all rows are in
+            const bool ok = thr == 0u || full || (double)funkey(thr) + delta_scale * sqrt(tot) < ks[k - 1];
+            out_unc[q] = ok ? 0 : 1;
+        }
     }
 }
 
@@ -575,7 +604,7 @@ static int pow2_at_least(int v) {
 struct KnnPlan {
     int L, nchunks, G, KC, npow2;
     long long S;
-    size_t slab_bytes, cand_bytes, sel_bytes, fin_bytes, tau_bytes, cnt_bytes, total;
+    size_t slab_bytes, cand_bytes, sel_bytes, fin_bytes, tau_bytes, cnt_bytes, total;  // tau_bytes: tau + sel_thr
 };
 
 static int default_cand(int k, int dtype) {
@@ -600,7 +629,7 @@ static KnnPlan plan(long long n_db, int nq, int k, int cand, int dtype) {
     p.cand_bytes = (size_t)nq * p.nchunks * p.KC * 4;
     p.sel_bytes = ((size_t)nq * p.KC * 4 + 255) / 256 * 256;
     p.fin_bytes = ((size_t)nq * p.npow2 * 8 + 255) / 256 * 256 + ((size_t)nq * p.npow2 * 4 + 255) / 256 * 256;
-    p.tau_bytes = ((size_t)nq * 4 + 255) / 256 * 256;
+    p.tau_bytes = ((size_t)nq * 8 + 255) / 256 * 256;
     p.cnt_bytes = ((size_t)nq * p.nchunks * 4 + 255) / 256 * 256;
     p.total = p.slab_bytes + 2 * ((p.cand_bytes + 255) / 256 * 256) + 2 * p.sel_bytes + p.fin_bytes + p.tau_bytes +
               p.cnt_bytes;
@@ -622,6 +651,14 @@ size_t rr_knn_workspace_bytes(long long n_db, int nq, int d, int k, int cand, in
 int rr_knn_topk(const void* db, const float* db_f32, long long n_db, const void* q, const float* q_f32, int nq, int d,
                 int k, int cand, long long idx_offset, double* out_scores, long long* out_idx, void* workspace,
                 size_t workspace_bytes, int dtype, void* stream) {
+    return rr_knn_topk_checked(db, db_f32, n_db, q, q_f32, nq, d, k, cand, idx_offset, out_scores, out_idx, workspace,
+                               workspace_bytes, dtype, 1.0f, nullptr, stream);
+}
+
+int rr_knn_topk_checked(const void* db, const float* db_f32, long long n_db, const void* q, const float* q_f32, int nq,
+                        int d, int k, int cand, long long idx_offset, double* out_scores, long long* out_idx,
+                        void* workspace, size_t workspace_bytes, int dtype, float db_norm_max, int* out_uncertain,
+                        void* stream) {
     if (n_db <= 0 || nq <= 0 || k <= 0) return fail(RR_EINVAL, "rr_knn_topk: empty problem");
     if (n_db > 0x7fffffffll) return fail(RR_EINVAL, "rr_knn_topk: shard rows must fit int32 (shard the database)");
     if (dtype != RR_BF16 && dtype != RR_F32 && dtype != RR_F16) return fail(RR_EINVAL, "rr_knn_topk: dtype");
@@ -642,6 +679,7 @@ int rr_knn_topk(const void* db, const float* db_f32, long long n_db, const void*
     double* fin_s = (double*)(fws + 2 * p.sel_bytes);
     int* fin_i = (int*)(fws + 2 * p.sel_bytes + ((size_t)nq * p.npow2 * 8 + 255) / 256 * 256);
     uint32_t* tau = (uint32_t*)(fws + 2 * p.sel_bytes + p.fin_bytes);
+    uint32_t* sel_thr = tau + nq;
     int* cnt = (int*)(fws + 2 * p.sel_bytes + p.fin_bytes + p.tau_bytes);
 
     static bool attr_done = false;
@@ -712,11 +750,16 @@ int rr_knn_topk(const void* db, const float* db_f32, long long n_db, const void*
     const size_t fin_lds = (size_t)p.npow2 * 12;
     if (fin_lds > 160 * 1024 - 4096) return fail(RR_EINVAL, "rr_knn_topk: candidate set exceeds LDS");
     hipLaunchKernelGGL(k_final_select, dim3(nq), dim3(SEL_THREADS), 0, s, cand_k, cand_i, cnt, p.nchunks, p.KC,
-                       sel_k, sel_i);
+                       sel_k, sel_i, sel_thr);
     hipLaunchKernelGGL(k_rescore, dim3((p.npow2 + 3) / 4, nq), dim3(256), 0, s, sel_i, p.KC, p.npow2, db_f32, q_f32, d,
                        fin_s, fin_i);
+    // screening error bound per unit ||q|| ||x||: input rounding of both
+    // operands (bf16 2^-9, fp16 2^-11 relative each; products exact in f32)
+    // plus f32 accumulation over d terms (d 2^-24)
+    const double in_eps = dtype == RR_BF16 ? 0x1p-8 + 0x1p-17 : dtype == RR_F16 ? 0x1p-10 + 0x1p-21 : 0.0;
+    const double delta_scale = (in_eps + d * 0x1p-24) * 1.001 * (db_norm_max > 0.f ? db_norm_max : 1.0);
     hipLaunchKernelGGL(k_final_sort, dim3(nq), dim3(SEL_THREADS), fin_lds, s, fin_s, fin_i, p.npow2, k, idx_offset,
-                       out_scores, out_idx);
+                       out_scores, out_idx, sel_thr, q_f32, d, delta_scale, out_uncertain);
     return check_launch("rr_knn_topk");
 }
 

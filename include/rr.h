@@ -200,6 +200,19 @@ int rr_knn_topk(const void* db, const float* db_f32, long long n_db,
                 long long idx_offset, double* out_scores, long long* out_idx,
                 void* workspace, size_t workspace_bytes, int dtype, void* stream);
 
+/* Same, with a certificate: out_uncertain[q] = 0 when the screening margin
+ * provably covers query q (every row outside the candidates has exact score
+ * below the returned k-th score: screening key + error bound, the bound from
+ * the screening dtype, d, ||q|| and db_norm_max = max ||db row||), 1 when a
+ * cluster tighter than the screening error straddles the candidate cut —
+ * re-search such queries with RR_F32 screening / more candidates
+ * (cirtorch.search.KnnIndex.search(verify=True) does). */
+int rr_knn_topk_checked(const void* db, const float* db_f32, long long n_db,
+                        const void* q, const float* q_f32, int nq, int d, int k, int cand,
+                        long long idx_offset, double* out_scores, long long* out_idx,
+                        void* workspace, size_t workspace_bytes, int dtype, float db_norm_max,
+                        int* out_uncertain, void* stream);
+
 /* Merge R per-shard top-k lists per query into one top-k by (score desc,
  * index asc).  in_*: [R][nq][k_in]; out_*: [nq][k].  Used after the RCCL
  * all-gather of per-shard results.  k_in*R <= 4096. */

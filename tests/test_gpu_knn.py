@@ -251,3 +251,33 @@ def test_knn_fused_graph_replay(cuda):
         assert torch.equal(i, ei) and torch.equal(s, es)
     ref_s, ref_i = ops.topk_exact(db.cpu().numpy(), q2.cpu().numpy(), 50)
     np.testing.assert_array_equal(index.search(q2, 50)[1].cpu().numpy(), ref_i)
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16", "fp32"])
+def test_knn_verify_tight_cluster(cuda, prec):
+    """600 near-copies of a query (scores within ~1e-4 of each other, tighter
+    than the bf16 / fp16 screening error) straddle the candidate cut: the
+    screening certificate flags that query (rr_knn_topk_checked), and
+    search(verify=True) re-searches it with float32 screening / more
+    candidates — the result equals the exact oracle.  Queries away from the
+    cluster certify."""
+    from cirtorch import _ops
+    from cirtorch.search import KnnIndex
+    from oracle import data, ops
+    d = 128
+    qq = data.unit_rows(4, d, seed=62)
+    db = data.unit_rows(170000, d, seed=64)
+    db[140000:140600] = qq[2] + 0.01 * data.unit_rows(600, d, seed=65)
+    db[140000:140600] /= np.linalg.norm(db[140000:140600], axis=1, keepdims=True)
+    ref_s, ref_i = ops.topk_exact(db, qq, 100)
+    index = KnnIndex(torch.from_numpy(db).to(cuda), prec)
+    q = torch.from_numpy(qq).to(cuda)
+    s, i = index.search(q, 100, verify=True)
+    np.testing.assert_array_equal(i.cpu().numpy(), ref_i)
+    np.testing.assert_allclose(s.cpu().numpy(), ref_s, rtol=0, atol=1e-12)
+    qs = _ops.cast_screen(q, index.dtype)
+    _, _, unc = _ops.knn_topk(index.db, index.db32, qs, q, 100, db_norm_max=index.norm_max())
+    unc = unc.cpu().numpy()
+    assert unc[0] == 0 and unc[1] == 0 and unc[3] == 0
+    if prec != "fp32":
+        assert unc[2] == 1
