@@ -41,7 +41,7 @@ static size_t slab_budget() {
 }
 typedef __attribute__((ext_vector_type(4))) float f32x4_knn_t;
 constexpr int MAX_SORT = 8192;
-constexpr int PREFIX_CHUNKS = 4;         // chunks through the slab path before the screening GEMM
+constexpr int PREFIX_CHUNKS = 8;         // chunks through the slab path before the screening GEMM
 int g_knn_fused = 1;                     // rr_set_tuning(RR_TUNE_KNN_FUSED)
 constexpr int TOPK_BINS = 2048;          // radix-select histogram (11-bit digits)
 
@@ -400,6 +400,32 @@ __global__ void __launch_bounds__(SEL_THREADS) k_final_select(const uint32_t* __
     if (threadIdx.x == 0) sel_thr[q] = thr;
 }
 
+// After the prefix chunks: tau[q] = the KC-th largest key of the whole prefix
+// pool (g0 x KC candidates).  The chunk selects only raised tau to the best
+// per-chunk KC-th key, which would let ~KC rows of every screened chunk
+// through (slot overflow); the pool's KC-th key lets ~KC / g0 through.
+// Still a valid bound: the pool holds KC keys >= it.
+__global__ void __launch_bounds__(SEL_THREADS) k_tau_refine(const uint32_t* __restrict__ cand_k, int nchunks, int g0,
+                                                            int KC, uint32_t* __restrict__ tau) {
+    __shared__ int smi[TOPK_BINS + 64];
+    __shared__ int nv;
+    const int q = blockIdx.x;
+    const uint32_t* ck = cand_k + (long long)q * nchunks * KC;
+    const int len = g0 * KC;
+    if (threadIdx.x == 0) nv = 0;
+    __syncthreads();
+    int c = 0;
+    for (int i = threadIdx.x; i < len; i += SEL_THREADS) c += ck[i] != 0u;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(&nv, c);
+    __syncthreads();
+    if (nv <= KC) return;  // block-uniform
+    int rem;
+    const uint32_t t = radix_kth<true>([&](int i) { return ck[i]; }, len, KC, smi, &rem);
+    if (threadIdx.x == 0 && t > tau[q]) tau[q] = t;
+}
+
 // tau[q] = 0 and the slot counts: chunks [0, g0) are filled whole by the
 // chunk select (count KC), the others start empty (screening epilogue).
 __global__ void k_knn_reset(uint32_t* __restrict__ tau, int* __restrict__ cnt, int nq, int nchunks, int g0, int KC,
@@ -731,6 +757,7 @@ int rr_knn_topk_checked(const void* db, const float* db_f32, long long n_db, con
                            rows, (int)r0, (int)(r0 / p.L), p.nchunks, p.KC, cand_k, cand_i, tau);
     }
     if (fused) {
+        hipLaunchKernelGGL(k_tau_refine, dim3(nq), dim3(SEL_THREADS), 0, s, cand_k, p.nchunks, g0, p.KC, tau);
         ConvArgs a = score_args(slab_rows, (int)(n_db - slab_rows));
         a.scr_tau = tau; a.scr_cnt = cnt; a.scr_k = cand_k; a.scr_i = cand_i;
         a.scr_L = p.L; a.scr_nchunks = p.nchunks; a.scr_KC = p.KC; a.scr_row0 = (int)slab_rows;

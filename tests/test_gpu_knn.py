@@ -204,7 +204,7 @@ def _fused_vs_slab(cuda, db, qq, k, prec):
 
 @pytest.mark.parametrize("prec", ["bf16", "fp16", "fp32"])
 def test_knn_fused_screen_stress(cuda, prec):
-    """Databases past the 4-chunk prefix (65536 rows), so the screening GEMM
+    """Databases past the 8-chunk prefix (131072 rows), so the screening GEMM
     epilogue runs: (a) scores rising row after row — every screened chunk
     overflows its slot and is rebuilt by the fix-up kernel; (b) blocks of the
     prefix duplicated in screened chunks — equal keys across the two paths,
@@ -221,7 +221,7 @@ def test_knn_fused_screen_stress(cuda, prec):
     rise = qq[:1] * t + data.unit_rows(180000, d, seed=63)
     rise = (rise / np.linalg.norm(rise, axis=1, keepdims=True)).astype(np.float32)
     dup = np.concatenate([base, base, base, base[:30000]], 0)                     # 150k rows
-    same = np.repeat(base[:1], 100000, 0)
+    same = np.repeat(base[:1], 150000, 0)
     plant = data.unit_rows(170000, d, seed=64)
     plant[140000:140600] = qq[2] + 0.3 * data.unit_rows(600, d, seed=65)   # scores ~0.96 +- 0.02
     plant[140000:140600] /= np.linalg.norm(plant[140000:140600], axis=1, keepdims=True)
@@ -240,7 +240,7 @@ def test_knn_fused_graph_replay(cuda):
     from cirtorch.search import KnnIndex
     from cirtorch.utils.graph import GraphedForward
     from oracle import data, ops
-    db = torch.from_numpy(data.unit_rows(120000, 256, seed=71)).to(cuda)
+    db = torch.from_numpy(data.unit_rows(200000, 256, seed=71)).to(cuda)
     q1 = torch.from_numpy(data.unit_rows(300, 256, seed=72)).to(cuda)
     q2 = torch.from_numpy(data.unit_rows(300, 256, seed=73)).to(cuda)
     index = KnnIndex(db, "bf16")
