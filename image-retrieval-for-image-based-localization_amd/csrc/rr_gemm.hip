@@ -923,7 +923,9 @@ bool gemm8_eligible(const ConvArgs& a, bool k1, int esz) {
     if ((long long)a.n * a.h * a.w_ * a.cin * 2 >= (1ll << 31) || 256ll * a.kp * 2 >= (1ll << 31)) return false;
     if ((a.flags & RR_CONV_PERM32) && a.cout % 32) return false;
     const long long ntiles = (long long)((a.P + 255) / 256) * ((a.cout + 255) / 256);
-    if (g_gemm8 == 1 && (a.P < 256 || ntiles < 2 * grid_cus() || a.cout % 256)) return false;
+    // (a partial last channel tile is negligible for long channel dims, e.g. the
+    // database rows of the kNN score GEMM)
+    if (g_gemm8 == 1 && (a.P < 256 || ntiles < 2 * grid_cus() || (a.cout % 256 && a.cout < 4096))) return false;
     return true;
 }
 

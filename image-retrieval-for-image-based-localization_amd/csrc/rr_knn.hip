@@ -41,7 +41,7 @@ static size_t slab_budget() {
 }
 typedef __attribute__((ext_vector_type(4))) float f32x4_knn_t;
 constexpr int MAX_SORT = 8192;
-constexpr int PREFIX_CHUNKS = 8;         // chunks through the slab path before the screening GEMM
+constexpr int PREFIX_CHUNKS = 4;         // chunks through the slab path before the screening GEMM
 int g_knn_fused = 1;                     // rr_set_tuning(RR_TUNE_KNN_FUSED)
 constexpr int TOPK_BINS = 2048;          // radix-select histogram (11-bit digits)
 

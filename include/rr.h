@@ -259,7 +259,7 @@ int rr_mutual_nn(const long long* nn12, int n1, const long long* nn21, int n2, l
  *                        (0 = all; e.g. half the chip for two concurrent streams)
  *   RR_TUNE_GEMM8        0 off, 1 auto, 2 forced: the 8-phase staggered 256x256 GEMM for eligible
  *                        16-bit 1x1 / tap-uniform convs and score GEMMs (default 1)
- *   RR_TUNE_KNN_FUSED    0/1 kNN screening in the score-GEMM epilogue after an 8-chunk
+ *   RR_TUNE_KNN_FUSED    0/1 kNN screening in the score-GEMM epilogue after a 4-chunk
  *                        prefix (default 1); 0 = every chunk through the score slab */
 enum rr_tune_key { RR_TUNE_GEMM_CONFIG = 0, RR_TUNE_GEMM_STAGES = 1, RR_TUNE_GEMM_WIDE = 2,
                    RR_TUNE_GEMM_ASTAT = 3, RR_TUNE_GEMM_XCD_MAP = 4, RR_TUNE_STREAM_1X1 = 5,

@@ -204,7 +204,7 @@ def _fused_vs_slab(cuda, db, qq, k, prec):
 
 @pytest.mark.parametrize("prec", ["bf16", "fp16", "fp32"])
 def test_knn_fused_screen_stress(cuda, prec):
-    """Databases past the 8-chunk prefix (131072 rows), so the screening GEMM
+    """Databases past the 4-chunk prefix (65536 rows), so the screening GEMM
     epilogue runs: (a) scores rising row after row — every screened chunk
     overflows its slot and is rebuilt by the fix-up kernel; (b) blocks of the
     prefix duplicated in screened chunks — equal keys across the two paths,
