@@ -245,7 +245,9 @@ def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], 
         e.record(main)
     state = {"slot": 0}
 
-    def run(part, items, pool):
+    outs = []  # (columns, descriptors) per chain; scattered into vecs once at the end
+
+    def run(part, items):
         """one same-size group of images -> their descriptor columns"""
         slot = state["slot"]
         if len(part) > 1:
@@ -254,8 +256,7 @@ def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], 
             if host is None:
                 host = pinned[key] = torch.empty((len(part),) + tuple(items[0].shape), dtype=items[0].dtype).pin_memory()
             copied[slot].synchronize()        # the previous H2D out of this host buffer has finished
-            # gather into the pinned buffer on the worker threads (tensor copies release the GIL)
-            list(pool.map(lambda j: host[j].copy_(items[j]), range(len(part))))
+            torch.stack(items, out=host)
         else:
             host = items[0][None]
         copy.wait_event(freed[slot])          # the extractor is done with this slot's device buffer
@@ -280,7 +281,9 @@ def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], 
                 acc = vs if acc is None else acc + vs
             v = (acc / len(ms)).pow(1.0 / msp)
             v = v / v.norm(dim=0, keepdim=True)
-        vecs[:, torch.tensor(part, device=dev)] = v.float()
+        # no host->device index copy here: a pageable copy would wait for the
+        # whole queued extraction and serialise host and device
+        outs.append((part, v.float()))
         freed[slot].record(main)
         state["slot"] = slot ^ 1
 
@@ -289,8 +292,7 @@ def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], 
         net.augment = None
     win = max(1, 8 * batch)
     try:
-        with ThreadPoolExecutor(max_workers=max(1, workers)) as pool, \
-                ThreadPoolExecutor(max_workers=max(1, workers)) as cpool, torch.no_grad():
+        with ThreadPoolExecutor(max_workers=max(1, workers)) as pool, torch.no_grad():
             def submit(w0):
                 return [pool.submit(_decode, images[i], image_size, bbxs[i] if bbxs is not None else None,
                                     transform, test_transform) for i in range(w0, min(n, w0 + win))]
@@ -304,7 +306,10 @@ def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], 
                 for js in groups.values():
                     for b0 in range(0, len(js), batch):
                         sub = js[b0:b0 + batch]
-                        run([w0 + j for j in sub], [decoded[j] for j in sub], cpool)
+                        run([w0 + j for j in sub], [decoded[j] for j in sub])
+            if outs:
+                cols = torch.tensor([c for part, _ in outs for c in part], dtype=torch.long).to(dev)
+                vecs[:, cols] = torch.cat([v for _, v in outs], dim=1)
     finally:
         net.augment = saved
     return vecs.cpu()
