@@ -25,6 +25,8 @@ for STEP in "$@"; do
         --output-format csv -- python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --latency 0 --pcie-steps 0 \
         > "$OUT/prof_bench.json" 2> "$OUT/prof.err")
       cat "$OUT/prof_bench.json" ;;
+    pmc)
+      bash "$ROOT/tools/pmc_round.sh" "gpurun_out/$TAG/pmc" ;;
     layers)
       timeout -k 10 300 python -u tools/layer_bench.py --batch 32 > "$OUT/layers_b32.txt" 2>&1
       cat "$OUT/layers_b32.txt" ;;
