@@ -22,7 +22,7 @@ for STEP in "$@"; do
       cat "$OUT/benchq.json" ;;
     prof)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run \
-        --output-format csv -- python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --latency 0 --pcie-steps 0 \
+        --output-format csv -- python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --no-extras --latency 0 --pcie-steps 0 \
         > "$OUT/prof_bench.json" 2> "$OUT/prof.err")
       cat "$OUT/prof_bench.json" ;;
     pmc)
