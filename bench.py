@@ -629,16 +629,26 @@ def main():
                    "roofline": {"bound": "mfma", "achieved": flops / tk / 1e12, "peak": peak, "unit": "TFLOP/s",
                                 "frac": flops / tk / 1e12 / peak, "traffic": None,
                                 "note": "per-rank screening GEMM FLOPs 2*Q*n_local*D / whole search time"}}
+            kpath = os.path.join(REPO, "profiles", "r02_pmc_knn_q%d.json" % args.knn_q)
+            if os.path.exists(kpath) and world == 1:
+                kt = json.load(open(kpath))
+                kc = kt.get("config", {})
+                if (kc.get("db_rows"), kc.get("dim"), kc.get("k"), kc.get("screen")) == (
+                        args.db_rows, args.dim, args.k, args.precision):
+                    knn["roofline"]["traffic"] = kt["hbm_bytes_per_search"]
+                    knn["roofline"]["traffic_note"] = (
+                        "HBM bytes of one search from rocprofv3 PMC (2 x FETCH_SIZE + WRITE_SIZE), %s, commit %s"
+                        % (os.path.relpath(kpath, REPO), kc.get("source_commit", "?")))
 
     traffic, traffic_note = None, "no PMC traffic file for this config"
-    tpath = os.path.join(REPO, "profiles", "r01_pmc_traffic.json")
+    tpath = os.path.join(REPO, "profiles", "r02_pmc_traffic.json")
     if os.path.exists(tpath):
         t = json.load(open(tpath))
         c = t.get("config", {})
         if (c.get("arch"), c.get("precision"), c.get("image")) == (args.arch, args.precision, [3, H, W]):
             traffic = t["hbm_bytes_per_image"] * B
             traffic_note = ("HBM bytes of the step's extractor dispatches from rocprofv3 PMC (2 x FETCH_SIZE + "
-                            "WRITE_SIZE, profiles/r01_pmc_traffic.json, %d-image forwards, commit %s)"
+                            "WRITE_SIZE, profiles/r02_pmc_traffic.json, %d-image forwards, commit %s)"
                             % (c.get("batch", 0), c.get("source_commit", "?")))
     # local-descriptor head: 2048 keypoints per image on an
     # R50 mod4-shaped bf16 map (1024 ch at H/16 x W/16), E = 128, + mutual NN of two images

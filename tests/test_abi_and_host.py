@@ -163,14 +163,28 @@ def test_whitenlearn_host_matches_reference_golden():
 
 
 def test_pmc_traffic_profile_matches_bench_defaults():
-    """bench.py reports roofline.traffic only when profiles/r01_pmc_traffic.json
+    """bench.py reports roofline.traffic only when profiles/r02_pmc_traffic.json
     was measured on its default workload; keep the file's config keys in step."""
     import json
     import os
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    t = json.load(open(os.path.join(root, "profiles", "r01_pmc_traffic.json")))
+    t = json.load(open(os.path.join(root, "profiles", "r02_pmc_traffic.json")))
     c = t["config"]
     assert (c["arch"], c["precision"], c["image"]) == ("resnet50", "bf16", [3, 768, 1024])
     assert c["batch"] == 128 and c.get("source_commit")
     # measured HBM bytes per image >= the algorithmic 808 MB of the body's layers
     assert 8.0e8 < t["hbm_bytes_per_image"] < 1.2e9
+
+
+def test_pmc_knn_traffic_profiles_match_bench_defaults():
+    """bench.py fills knn.roofline.traffic from profiles/r02_pmc_knn_q<Q>.json
+    only for its default database (1M x 2048 bf16, k=100)."""
+    import json
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for q in (128, 1024):
+        t = json.load(open(os.path.join(root, "profiles", "r02_pmc_knn_q%d.json" % q)))
+        c = t["config"]
+        assert (c["q"], c["db_rows"], c["dim"], c["k"], c["screen"]) == (q, 1000000, 2048, 100, "bf16")
+        # at least one pass over the bf16 database (4.096 GB)
+        assert 4.0e9 < t["hbm_bytes_per_search"] < 2.0e10
