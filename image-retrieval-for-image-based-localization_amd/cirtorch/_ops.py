@@ -77,8 +77,9 @@ def conv1x1_pair(x, w3, scale3, shift3, residual, leaky3, slope3, w1, scale1, sh
     """Fused y = act3(conv1x1(x, w3)*scale3 + shift3 + shortcut); z = act1(conv1x1(y, w1)*scale1 + shift1)
     (conv3 of one bottleneck block + conv1 of the next, cirtorch/backbones/misc.py:166-203).
     shortcut = residual, or with residual=None and proj=(xp, wp, scalep, shiftp) the block's 1x1
-    projection proj_bn(proj_conv(xp)) computed in the same pass.
-    x: [N, H, W, 64] bf16, PERM32-packed weights; returns (y [N, H, W, 256], z [N, H, W, c_out])."""
+    projection proj_bn(proj_conv(xp)) computed in the same pass (64 -> 256 boundaries only).
+    x: [N, H, W, 64] or [N, H, W, 128] bf16 / fp16, PERM32-packed weights; returns
+    (y [N, H, W, 256 | 512], z [N, H, W, c_out])."""
     E.require_gpu(x, w3, residual, w1)
     n, h, w, c = x.shape
     c_mid = w3.shape[0]

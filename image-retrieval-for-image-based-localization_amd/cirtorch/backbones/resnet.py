@@ -253,13 +253,19 @@ class ResNet(nn.Module):
                 and proj.w.shape[1] == 64 and not proj.leaky)
 
     def _pairable(self, last, nxt):
-        """conv3 of a 64->256 bottleneck followed by a stride-1 1x1 conv1 (256 -> 64/128):
-        one fused rr_conv1x1_pair launch (bf16 / fp16)."""
+        """conv3 of a bottleneck followed by a stride-1 1x1 conv1 of the next block: one fused
+        rr_conv1x1_pair launch (bf16 / fp16) for the 64 -> 256 -> 64/128 boundaries (mod2) and
+        the 128 -> 512 -> 128 ones (mod3; RR_PAIR_MID=0 keeps those as two launches)."""
         if nxt is None or self.engine_dtype == torch.float32 or os.environ.get("RR_PAIR_FUSED", "1") == "0":
             return False
-        return (last.kh == 1 and last.stride == 1 and last.perm and last.c_out == 256 and last.w.shape[1] == 64
-                and nxt.kh == 1 and nxt.stride == 1 and nxt.pad == 0 and nxt.perm and nxt.w.shape[1] == 256
-                and nxt.c_out in (64, 128))
+        if not (last.kh == 1 and last.stride == 1 and last.perm and nxt.kh == 1 and nxt.stride == 1
+                and nxt.pad == 0 and nxt.perm):
+            return False
+        if last.c_out == 256 and last.w.shape[1] == 64:
+            return nxt.w.shape[1] == 256 and nxt.c_out in (64, 128)
+        if last.c_out == 512 and last.w.shape[1] == 128 and os.environ.get("RR_PAIR_MID", "1") != "0":
+            return nxt.w.shape[1] == 512 and nxt.c_out == 128
+        return False
 
 
 _NETS = {

@@ -28,6 +28,8 @@
 // leaky_relu (cirtorch/utils/misc.py:175-235).
 #include "rr_internal.h"
 
+#include <type_traits>
+
 namespace rr {
 
 namespace {
@@ -84,7 +86,7 @@ struct TileC {
 
 template <int TC, int TH, int TW, int WC, int WP, bool ARES, int NSA, typename HT>
 __global__ void __launch_bounds__(64 * WC * WP) k_conv3x3(ConvArgs a, int tiles_w, int tiles_hw, int tiles_c,
-                                                         int ntiles) {
+                                                         int ntiles, int g_pipe) {
     constexpr int NW = WC * WP, NT = 64 * NW;
     constexpr int TP = TH * TW;
     constexpr int PC = TW + 2, NPIX = (TH + 2) * PC;
@@ -120,6 +122,7 @@ __global__ void __launch_bounds__(64 * WC * WP) k_conv3x3(ConvArgs a, int tiles_
             sH[i] = aff ? a.shift[i] : 0.f;
         }
     }
+    __syncthreads();  // affine visible to every wave (read into VGPRs by the overlapped epilogue)
     const int my_tiles = (int)blockIdx.x < ntiles ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
     if (my_tiles == 0) return;
 
@@ -173,63 +176,81 @@ __global__ void __launch_bounds__(64 * WC * WP) k_conv3x3(ConvArgs a, int tiles_
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = (pf32x4_t){0.f, 0.f, 0.f, 0.f};
 
+    // A / B fragments of half-step hs (channels 32*hs .. +31 of the 64-channel
+    // K-step) at tap offset toff, and the FM x FN MFMAs on them
+    auto frag_load = [&](const char* As, const char* Ps, int toff, int hs, uint4 (&fa)[FM], uint4 (&fb)[FN]) {
+        const int ch = kq + 4 * hs;
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+            fa[i] = *reinterpret_cast<const uint4*>(As + (arow0 + i * 16) * 128 + ((ch ^ (r16 & 7)) << 4));
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+            const int q = bq[j] + toff;
+            fb[j] = *reinterpret_cast<const uint4*>(Ps + q * 128 + ((ch ^ (q & 7)) << 4));
+        }
+    };
+    auto frag_mfma = [&](const uint4 (&fa)[FM], const uint4 (&fb)[FN]) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+                acc[i][j] = H16<HT>::mfma(fa[i], fb[j], acc[i][j]);
+    };
     auto mfma_step = [&](const char* As, const char* Ps, int toff) {
 #pragma unroll
         for (int hs = 0; hs < 2; ++hs) {
-            const int ch = kq + 4 * hs;
             uint4 fa[FM], fb[FN];
-#pragma unroll
-            for (int i = 0; i < FM; ++i)
-                fa[i] = *reinterpret_cast<const uint4*>(As + (arow0 + i * 16) * 128 + ((ch ^ (r16 & 7)) << 4));
-#pragma unroll
-            for (int j = 0; j < FN; ++j) {
-                const int q = bq[j] + toff;
-                fb[j] = *reinterpret_cast<const uint4*>(Ps + q * 128 + ((ch ^ (q & 7)) << 4));
-            }
-#pragma unroll
-            for (int i = 0; i < FM; ++i)
-#pragma unroll
-                for (int j = 0; j < FN; ++j)
-                    acc[i][j] = H16<HT>::mfma(fa[i], fb[j], acc[i][j]);
+            frag_load(As, Ps, toff, hs, fa, fb);
+            frag_mfma(fa, fb);
         }
     };
-
     bf16_t* __restrict__ Y = (bf16_t*)a.y;
     const bool leaky = a.act == RR_ACT_LEAKY;
     const float slope = a.slope;
     // PERM32 rows: a lane's fragment pair (2*i2, 2*i2+1) holds 8 consecutive
     // output channels of one pixel -> one 16-B store; exactly NST stores.
+    // one 16-B store of the epilogue: fragment pair (2*i2, 2*i2+1) x pixel
+    // fragment j of accumulators `ac`, BN affine (sc, sh: this lane's 8 channels)
+    auto store_one = [&](const TileC& tc, const pf32x4_t (&ac)[FM][FN], int i2, int j, const float (&sc)[8],
+                         const float (&sh)[8]) {
+        const int c = tc.ct * TC + wc * (TC / WC) + 32 * i2 + 8 * kq;
+        const int p = wp * (TP / WP) + j * 16 + r16;
+        const long long pix = ((long long)tc.img * H + tc.oh0 + p / TW) * W + tc.ow0 + p % TW;
+        float v[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            v[r] = ac[2 * i2][j][r] * sc[r] + sh[r];
+            v[4 + r] = ac[2 * i2 + 1][j][r] * sc[4 + r] + sh[4 + r];
+        }
+        if (leaky) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * slope;
+        }
+        uint4 o;
+        o.x = H16<HT>::pack2(v[0], v[1]);
+        o.y = H16<HT>::pack2(v[2], v[3]);
+        o.z = H16<HT>::pack2(v[4], v[5]);
+        o.w = H16<HT>::pack2(v[6], v[7]);
+        *reinterpret_cast<uint4*>(Y + pix * a.ldy + c) = o;
+    };
+    auto load_affine = [&](int ct, int i2, float (&sc)[8], float (&sh)[8]) {
+        const int c = ct * TC + wc * (TC / WC) + 32 * i2 + 8 * kq;
+        const float4 s0 = *reinterpret_cast<const float4*>(sS + c);
+        const float4 s1 = *reinterpret_cast<const float4*>(sS + c + 4);
+        const float4 h0 = *reinterpret_cast<const float4*>(sH + c);
+        const float4 h1 = *reinterpret_cast<const float4*>(sH + c + 4);
+        sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w; sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
+        sh[0] = h0.x; sh[1] = h0.y; sh[2] = h0.z; sh[3] = h0.w; sh[4] = h1.x; sh[5] = h1.y; sh[6] = h1.z; sh[7] = h1.w;
+    };
+    // PERM32 rows: a lane's fragment pair (2*i2, 2*i2+1) holds 8 consecutive
+    // output channels of one pixel -> one 16-B store; exactly NST stores.
     auto epilogue = [&](const TileC& tc) {
 #pragma unroll
         for (int i2 = 0; i2 < FM / 2; ++i2) {
-            const int c = tc.ct * TC + wc * (TC / WC) + 32 * i2 + 8 * kq;
-            const float4 s0 = *reinterpret_cast<const float4*>(sS + c);
-            const float4 s1 = *reinterpret_cast<const float4*>(sS + c + 4);
-            const float4 h0 = *reinterpret_cast<const float4*>(sH + c);
-            const float4 h1 = *reinterpret_cast<const float4*>(sH + c + 4);
-            const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-            const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+            float sc[8], sh[8];
+            load_affine(tc.ct, i2, sc, sh);
 #pragma unroll
-            for (int j = 0; j < FN; ++j) {
-                const int p = wp * (TP / WP) + j * 16 + r16;
-                const long long pix = ((long long)tc.img * H + tc.oh0 + p / TW) * W + tc.ow0 + p % TW;
-                float v[8];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    v[r] = acc[2 * i2][j][r] * sc[r] + sh[r];
-                    v[4 + r] = acc[2 * i2 + 1][j][r] * sc[4 + r] + sh[4 + r];
-                }
-                if (leaky) {
-#pragma unroll
-                    for (int r = 0; r < 8; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * slope;
-                }
-                uint4 o;
-                o.x = H16<HT>::pack2(v[0], v[1]);
-                o.y = H16<HT>::pack2(v[2], v[3]);
-                o.z = H16<HT>::pack2(v[4], v[5]);
-                o.w = H16<HT>::pack2(v[6], v[7]);
-                *reinterpret_cast<uint4*>(Y + pix * a.ldy + c) = o;
-            }
+            for (int j = 0; j < FN; ++j) store_one(tc, acc, i2, j, sc, sh);
         }
 #pragma unroll
         for (int i = 0; i < FM; ++i)
@@ -244,19 +265,113 @@ __global__ void __launch_bounds__(64 * WC * WP) k_conv3x3(ConvArgs a, int tiles_
 #pragma unroll
         for (int tap = 0; tap < 9; ++tap) w_dma(0, tap, 0, lds0 + tap * AST);
         for (int d = wave; d < NDP; d += NW) patch_dma(cur, 0, 0, d);
-        for (int lt = 0; lt < my_tiles; ++lt) {
-            // patch(lt) landed (older than the previous tile's NST epilogue stores)
-            if (lt == 0) pwait_barrier<0>();
-            else pwait_barrier<NST>();
-            if (lt + 1 < my_tiles) {
-                const TileC nxt = tile_of(lt + 1);
-                for (int d = wave; d < NDP; d += NW) patch_dma(nxt, 0, (lt + 1) & 1, d);
-            }
-            const char* Ps = smem + ABYTES + (lt & 1) * PBYTES;
+        if (g_pipe) {
+            // Epilogue overlap: tile lt's stores are computed from a copy of its
+            // accumulators (accP) during tile lt + 1's MFMAs, one store after
+            // every few half-steps, so the VALU / store issue of the epilogue
+            // hides under the matrix pipe instead of idling it between tiles
+            // (all waves reach the epilogue together: one barrier per tile).
+            // Branch-free activation: leaky(v) = max(v, slope * v) for slope in
+            // [0, 1] (host-checked; identity = slope 1), bit-equal to the select form.
+            pf32x4_t accP[FM][FN];
+            float esc[FM / 2][8], esh[FM / 2][8];  // one channel tile: the affine stays in VGPRs
+            const float sl = leaky ? slope : 1.f;
+            auto store_bf = [&](const TileC& tc, int i2, int j) {
+                const int c = wc * (TC / WC) + 32 * i2 + 8 * kq;
+                const int p = wp * (TP / WP) + j * 16 + r16;
+                const long long pix = ((long long)tc.img * H + tc.oh0 + p / TW) * W + tc.ow0 + p % TW;
+                float v[8];
 #pragma unroll
-            for (int tap = 0; tap < 9; ++tap) mfma_step(smem + tap * AST, Ps, (tap / 3) * PC + tap % 3);
-            epilogue(cur);
-            if (lt + 1 < my_tiles) cur = tile_of(lt + 1);
+                for (int r = 0; r < 4; ++r) {
+                    v[r] = accP[2 * i2][j][r] * esc[i2][r] + esh[i2][r];
+                    v[4 + r] = accP[2 * i2 + 1][j][r] * esc[i2][4 + r] + esh[i2][4 + r];
+                }
+#pragma unroll
+                for (int r = 0; r < 8; ++r) v[r] = fmaxf(v[r], v[r] * sl);
+                uint4 o;
+                o.x = H16<HT>::pack2(v[0], v[1]);
+                o.y = H16<HT>::pack2(v[2], v[3]);
+                o.z = H16<HT>::pack2(v[4], v[5]);
+                o.w = H16<HT>::pack2(v[6], v[7]);
+                *reinterpret_cast<uint4*>(Y + pix * a.ldy + c) = o;
+            };
+            TileC prev = cur;
+            auto tile_body = [&](auto has_prev, int lt) {
+                const char* Ps = smem + ABYTES + (lt & 1) * PBYTES;
+                constexpr int GAP = 18 / NST > 0 ? 18 / NST : 1;
+                // per-tile opaque copies of the patch pixel indices: the 18 x FN fragment
+                // addresses are derived inside the tile instead of being hoisted out of
+                // the tile loop as loop invariants (they would not fit beside accP)
+                int bql[FN];
+#pragma unroll
+                for (int j = 0; j < FN; ++j) {
+                    bql[j] = bq[j];
+                    asm volatile("" : "+v"(bql[j]));
+                }
+#pragma unroll
+                for (int s = 0; s < 18; ++s) {
+                    const int tap = s >> 1;
+                    uint4 fa[FM], fb[FN];
+                    {
+                        const int ch = kq + 4 * (s & 1), toff = (tap / 3) * PC + tap % 3;
+                        const char* As = smem + tap * AST;
+#pragma unroll
+                        for (int i = 0; i < FM; ++i)
+                            fa[i] = *reinterpret_cast<const uint4*>(As + (arow0 + i * 16) * 128 + ((ch ^ (r16 & 7)) << 4));
+#pragma unroll
+                        for (int j = 0; j < FN; ++j) {
+                            const int q = bql[j] + toff;
+                            fb[j] = *reinterpret_cast<const uint4*>(Ps + q * 128 + ((ch ^ (q & 7)) << 4));
+                        }
+                    }
+                    frag_mfma(fa, fb);
+                    if constexpr (decltype(has_prev)::value) {
+                        if (s % GAP == GAP - 1 && s / GAP < NST) store_bf(prev, (s / GAP) / FN, (s / GAP) % FN);
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < FM; ++i)
+#pragma unroll
+                    for (int j = 0; j < FN; ++j) {
+                        accP[i][j] = acc[i][j];
+                        acc[i][j] = (pf32x4_t){0.f, 0.f, 0.f, 0.f};
+                    }
+            };
+            for (int lt = 0; lt < my_tiles; ++lt) {
+                // patch(lt) landed; from lt = 2 on the NST stores of tile lt - 2 (issued
+                // during tile lt - 1, after patch(lt)'s DMA) may stay in flight
+                if (lt <= 1) pwait_barrier<0>();
+                else pwait_barrier<NST>();
+                if (lt == 0) {
+#pragma unroll
+                    for (int i2 = 0; i2 < FM / 2; ++i2) load_affine(0, i2, esc[i2], esh[i2]);
+                }
+                if (lt + 1 < my_tiles) {
+                    const TileC nxt = tile_of(lt + 1);
+                    for (int d = wave; d < NDP; d += NW) patch_dma(nxt, 0, (lt + 1) & 1, d);
+                }
+                if (lt == 0) tile_body(std::false_type{}, lt);
+                else tile_body(std::true_type{}, lt);
+                prev = cur;
+                if (lt + 1 < my_tiles) cur = tile_of(lt + 1);
+            }
+#pragma unroll
+            for (int e = 0; e < NST; ++e) store_bf(prev, e / FN, e % FN);
+        } else {
+            for (int lt = 0; lt < my_tiles; ++lt) {
+                // patch(lt) landed (older than the previous tile's NST epilogue stores)
+                if (lt == 0) pwait_barrier<0>();
+                else pwait_barrier<NST>();
+                if (lt + 1 < my_tiles) {
+                    const TileC nxt = tile_of(lt + 1);
+                    for (int d = wave; d < NDP; d += NW) patch_dma(nxt, 0, (lt + 1) & 1, d);
+                }
+                const char* Ps = smem + ABYTES + (lt & 1) * PBYTES;
+#pragma unroll
+                for (int tap = 0; tap < 9; ++tap) mfma_step(smem + tap * AST, Ps, (tap / 3) * PC + tap % 3);
+                epilogue(cur);
+                if (lt + 1 < my_tiles) cur = tile_of(lt + 1);
+            }
         }
     } else {
         // steps (tile, chunk, tap); weight K-steps through an NSA-stage ring, one
@@ -323,18 +438,24 @@ __global__ void __launch_bounds__(64 * WC * WP) k_conv3x3(ConvArgs a, int tiles_
     }
 }
 
+}  // namespace
+int g_conv3_pipe = 1;  // rr_set_tuning(RR_TUNE_CONV3_PIPE): 1 software-pipelined A-stationary tiles, 0 compiler schedule
+namespace {
+
 template <int TC, int TH, int TW, int WC, int WP, bool ARES, int NSA = 2>
 void launch_c3(const ConvArgs& a, hipStream_t s, bool f16) {
     const int tiles_w = a.w_ / TW, tiles_h = a.h / TH, tiles_c = a.cout / TC;
     const long long ntl = (long long)a.n * tiles_h * tiles_w * tiles_c;
     const int cus = grid_cus();
     const int grid = (int)(ntl < cus ? ntl : cus);
+    // the overlapped epilogue's branch-free activation needs slope in [0, 1]
+    const int pipe = g_conv3_pipe && (a.act != RR_ACT_LEAKY || (a.slope >= 0.f && a.slope <= 1.f));
     if (f16)
         hipLaunchKernelGGL((k_conv3x3<TC, TH, TW, WC, WP, ARES, NSA, f16_t>), dim3(grid), dim3(64 * WC * WP), 0, s, a,
-                           tiles_w, tiles_w * tiles_h, tiles_c, (int)ntl);
+                           tiles_w, tiles_w * tiles_h, tiles_c, (int)ntl, pipe);
     else
         hipLaunchKernelGGL((k_conv3x3<TC, TH, TW, WC, WP, ARES, NSA, bf16_t>), dim3(grid), dim3(64 * WC * WP), 0, s, a,
-                           tiles_w, tiles_w * tiles_h, tiles_c, (int)ntl);
+                           tiles_w, tiles_w * tiles_h, tiles_c, (int)ntl, pipe);
 }
 
 }  // namespace

@@ -413,6 +413,237 @@ __global__ void __launch_bounds__(512) k_stream_pair(PairArgs a) {
 }
 
 
+// ---------------------------------------------------------------------------
+// Fused bottleneck boundary of the 128/512-channel stage (ResNet-50/101/152
+// mod3): block i's conv3 (1x1, 128 -> 512, BN, + residual, activation) and
+// block i+1's conv1 (1x1, 512 -> 128, BN, activation) in one pass, so the
+// 512-channel map y is written once and never read back (-1 KiB per pixel).
+// The weights (128 KiB + 128 KiB) do not fit in LDS beside the tiles, so they
+// live in VGPRs for the whole launch: wave w holds W3 rows 64w..64w+63 (4 x 4
+// fragments) and W1 rows 16w..16w+15 (16 fragments), 128 VGPRs.  Per tile of
+// TP = 64 pixels (persistent blocks, one per CU):
+//   * x tile [64][128] (16 KiB) and residual tile [64][512] (64 KiB) arrive by
+//     LDS-DMA (buffer_load ... lds), the residual one tile ahead into the
+//     second of two buffers, x during stage 2 of the previous tile;
+//   * stage 1: y = act3(W3 x * s3 + h3 + r) per wave for its 64 channels; y
+//     goes to HBM and, in place of the residual, into the LDS tile;
+//   * stage 2: z = act1(W1 y * s1 + h1) with y read back from LDS (K = 512).
+// LDS images are [pixel][16-B chunk] with the chunk XOR (pixel & 15) swizzle
+// (applied on the DMA source side): every ds_read_b128 lane group of a B
+// fragment hits 16 distinct 16-B bank groups.  MFMA accumulation order per
+// element equals the two unfused k_stream1x1 launches (K-steps in order), so
+// y and z are bit-identical to them.
+typedef __attribute__((ext_vector_type(4))) int si32x4_t;
+
+__device__ __forceinline__ void sdma16(si32x4_t rsrc, unsigned voff, unsigned lds_addr) {
+    unsigned keep;
+    lds_addr = __builtin_amdgcn_readfirstlane(lds_addr);
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %3\n\t"
+        "s_nop 4\n\t"
+        "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(rsrc), "s"(lds_addr)
+        : "memory");
+}
+__device__ __forceinline__ si32x4_t srsrc(const void* base, unsigned bytes) {
+    const unsigned long long b = (unsigned long long)base;
+    si32x4_t r;
+    r.x = __builtin_amdgcn_readfirstlane((int)(unsigned)b);
+    r.y = __builtin_amdgcn_readfirstlane((int)((unsigned)(b >> 32) & 0xFFFFu));
+    r.z = __builtin_amdgcn_readfirstlane((int)bytes);  // reads past the end return zeros
+    r.w = 0x00020000;
+    return r;
+}
+
+struct PairMidArgs {
+    const bf16_t* x;    // [P][128]
+    const bf16_t* w3;   // [512][128] PERM32 rows
+    const float *s3, *h3;
+    const bf16_t* res;  // [P][512]
+    const bf16_t* w1;   // [128][512] PERM32 rows
+    const float *s1, *h1;
+    bf16_t* y;          // [P][512]
+    bf16_t* z;          // [P][128]
+    long long P;
+    int act3, act1;
+    float slope3, slope1;
+};
+
+template <typename H>
+__global__ void __launch_bounds__(512, 1) k_pair_mid(PairMidArgs a) {
+    constexpr int K3 = 128, C3 = 512, C1 = 128, TP = 64;
+    constexpr int XB = TP * K3 * 2, RB = TP * C3 * 2;  // 16 KiB, 64 KiB
+    __shared__ __attribute__((aligned(1024))) char smem[2 * RB + XB];
+    __shared__ __attribute__((aligned(16))) float sS3[C3], sH3[C3], sS1[C1], sH1[C1];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r16 = lane & 15, kq = lane >> 4;
+    for (int i = tid; i < C3; i += 512) {
+        sS3[i] = a.s3[i];
+        sH3[i] = a.h3[i];
+    }
+    if (tid < C1) {
+        sS1[tid] = a.s1[tid];
+        sH1[tid] = a.h1[tid];
+    }
+    // weight fragments -> VGPRs (A operand: lane holds k = 32 kk + 8 kq .. + 7 of row r16)
+    uint4 a3[4][4], a1[16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+            a3[i][kk] = *reinterpret_cast<const uint4*>(a.w3 + (long long)(64 * wave + 16 * i + r16) * K3 + 32 * kk + 8 * kq);
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk)
+        a1[kk] = *reinterpret_cast<const uint4*>(a.w1 + (long long)(16 * wave + r16) * C3 + 32 * kk + 8 * kq);
+    __syncthreads();
+
+    const long long P = a.P;
+    const int ntiles = (int)((P + TP - 1) / TP);
+    const int t0 = (int)blockIdx.x, G = (int)gridDim.x;
+    if (t0 >= ntiles) return;
+    const si32x4_t rsX = srsrc(a.x, (unsigned)(P * K3 * 2));
+    const si32x4_t rsR = srsrc(a.res, (unsigned)(P * C3 * 2));
+    const unsigned lds0 = (unsigned)(unsigned long long)smem;
+    const unsigned ldsX = lds0 + 2 * RB;
+    // x tile: 16 wave-instructions of 4 pixels x 256 B (2 per wave)
+    auto dma_x = [&](int t) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int d = 2 * wave + u, px = 4 * d + (lane >> 4), slot = lane & 15;
+            const unsigned off = (unsigned)(((long long)t * TP + px) * (K3 * 2)) + (unsigned)((slot ^ (px & 15)) << 4);
+            sdma16(rsX, off, ldsX + d * 1024);
+        }
+    };
+    // residual tile: 64 wave-instructions of one pixel x 1 KiB (8 per wave)
+    auto dma_r = [&](int t, int buf) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int px = 8 * wave + u;
+            const unsigned off = (unsigned)(((long long)t * TP + px) * (C3 * 2)) + (unsigned)((lane ^ (px & 15)) << 4);
+            sdma16(rsR, off, lds0 + buf * RB + px * 1024);
+        }
+    };
+    const bool leaky3 = a.act3 == RR_ACT_LEAKY, leaky1 = a.act1 == RR_ACT_LEAKY;
+
+    dma_r(t0, 0);
+    dma_x(t0);
+    for (int k = 0, t = t0; t < ntiles; ++k, t += G) {
+        const int cur = k & 1;
+        const bool more = t + G < ntiles;
+        // x(t), r(t) landed; only the previous tile's 4 z stores may stay in flight
+        if (k == 0) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+        if (more) dma_r(t + G, cur ^ 1);
+        const char* X = smem + 2 * RB;
+        char* RY = smem + cur * RB;
+        // ---- stage 1: y = act3(W3 x * s3 + h3 + r), one 32-channel pair at a time
+#pragma unroll
+        for (int i2 = 0; i2 < 2; ++i2) {
+            h16_f32x4_t acc[2][4];
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[h][j] = (h16_f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                uint4 bx[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int px = 16 * j + r16;
+                    bx[j] = *reinterpret_cast<const uint4*>(X + px * (K3 * 2) + ((((4 * kk + kq) ^ (px & 15))) << 4));
+                }
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) acc[h][j] = H16<H>::mfma(a3[2 * i2 + h][kk], bx[j], acc[h][j]);
+            }
+            const int c = 64 * wave + 32 * i2 + 8 * kq;  // 8 consecutive channels of this lane (PERM32)
+            const int chunk = c >> 3;
+            const float4 sc0 = *reinterpret_cast<const float4*>(sS3 + c);
+            const float4 sc1 = *reinterpret_cast<const float4*>(sS3 + c + 4);
+            const float4 sh0 = *reinterpret_cast<const float4*>(sH3 + c);
+            const float4 sh1 = *reinterpret_cast<const float4*>(sH3 + c + 4);
+            const float sc[8] = {sc0.x, sc0.y, sc0.z, sc0.w, sc1.x, sc1.y, sc1.z, sc1.w};
+            const float sh[8] = {sh0.x, sh0.y, sh0.z, sh0.w, sh1.x, sh1.y, sh1.z, sh1.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int px = 16 * j + r16;
+                uint4* slot = reinterpret_cast<uint4*>(RY + px * (C3 * 2) + ((chunk ^ (px & 15)) << 4));
+                const uint4 q = *slot;
+                const unsigned w4[4] = {q.x, q.y, q.z, q.w};
+                float v[8];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    v[r] = acc[0][j][r] * sc[r] + sh[r];
+                    v[4 + r] = acc[1][j][r] * sc[4 + r] + sh[4 + r];
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    v[2 * r] += H16<H>::lo(w4[r]);
+                    v[2 * r + 1] += H16<H>::hi(w4[r]);
+                }
+                if (leaky3) {
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * a.slope3;
+                }
+                uint4 o;
+                o.x = H16<H>::pack2(v[0], v[1]);
+                o.y = H16<H>::pack2(v[2], v[3]);
+                o.z = H16<H>::pack2(v[4], v[5]);
+                o.w = H16<H>::pack2(v[6], v[7]);
+                *slot = o;
+                const long long p = (long long)t * TP + px;
+                if (p < P) *reinterpret_cast<uint4*>(a.y + p * C3 + c) = o;
+            }
+        }
+        // y tile complete in LDS; x buffer free
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (more) dma_x(t + G);
+        // ---- stage 2: z = act1(W1 y * s1 + h1), K = 512 from the LDS y tile
+        h16_f32x4_t zacc[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) zacc[j] = (h16_f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk) {
+            uint4 by[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int px = 16 * j + r16;
+                by[j] = *reinterpret_cast<const uint4*>(RY + px * (C3 * 2) + ((((4 * kk + kq) ^ (px & 15))) << 4));
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) zacc[j] = H16<H>::mfma(a1[kk], by[j], zacc[j]);
+        }
+        {
+            // packed rows 16w + 4kq + r = channels 32 (w >> 1) + 8 kq + 4 (w & 1) + r
+            const int c = 32 * (wave >> 1) + 8 * kq + 4 * (wave & 1);
+            const float4 sc = *reinterpret_cast<const float4*>(sS1 + c);
+            const float4 sh = *reinterpret_cast<const float4*>(sH1 + c);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float v[4] = {zacc[j][0] * sc.x + sh.x, zacc[j][1] * sc.y + sh.y, zacc[j][2] * sc.z + sh.z,
+                              zacc[j][3] * sc.w + sh.w};
+                if (leaky1) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * a.slope1;
+                }
+                uint2 o;
+                o.x = H16<H>::pack2(v[0], v[1]);
+                o.y = H16<H>::pack2(v[2], v[3]);
+                const long long p = (long long)t * TP + 16 * j + r16;
+                if (p < P) *reinterpret_cast<uint2*>(a.z + p * C1 + c) = o;
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+
 template <int TC, int K, int FN, int D, int NW, typename H>
 void launch_s_t(const ConvArgs& a, hipStream_t s) {
     const int g_stream_cus = grid_cus();
@@ -486,11 +717,14 @@ extern "C" int rr_conv1x1_pair(const void* x, long long p, int c_in, const void*
                                const float* scale1, const float* shift1, int c_out, int act1, float slope1, void* y,
                                void* z, int dtype, void* stream) {
     if (dtype != RR_BF16 && dtype != RR_F16) return fail(RR_EINVAL, "rr_conv1x1_pair: bf16 / fp16 only");
-    if (c_in != 64 || c_mid != 256 || (c_out != 64 && c_out != 128))
-        return fail(RR_EINVAL, "rr_conv1x1_pair: shapes (c_in 64, c_mid 256, c_out 64|128) only");
+    const bool stage2 = c_in == 64 && c_mid == 256 && (c_out == 64 || c_out == 128);
+    const bool stage3 = c_in == 128 && c_mid == 512 && c_out == 128;
+    if (!stage2 && !stage3)
+        return fail(RR_EINVAL, "rr_conv1x1_pair: shapes (c_in 64, c_mid 256, c_out 64|128) or (128, 512, 128) only");
     if (!x || !w3 || !scale3 || !shift3 || !w1 || !scale1 || !shift1 || !y || !z)
         return fail(RR_EINVAL, "rr_conv1x1_pair: null pointer");
     const bool proj = residual == nullptr;
+    if (proj && stage3) return fail(RR_EINVAL, "rr_conv1x1_pair: the 128/512 boundary needs a residual");
     if (proj && (!xp || !wp || !scalep || !shiftp))
         return fail(RR_EINVAL, "rr_conv1x1_pair: either residual or the projection (xp, wp, scalep, shiftp) is required");
     if (proj && ((((uintptr_t)xp) | ((uintptr_t)wp)) & 15))
@@ -502,6 +736,24 @@ extern "C" int rr_conv1x1_pair(const void* x, long long p, int c_in, const void*
     if (act3 != RR_ACT_IDENTITY && act3 != RR_ACT_LEAKY) return fail(RR_EINVAL, "rr_conv1x1_pair: act3");
     if (act1 != RR_ACT_IDENTITY && act1 != RR_ACT_LEAKY) return fail(RR_EINVAL, "rr_conv1x1_pair: act1");
     const int g_pair_cus = grid_cus();
+    hipStream_t s = as_stream(stream);
+    if (stage3) {
+        // pixel chunks of 2^20 (the residual buffer resource addresses 1 GiB with 32-bit offsets)
+        constexpr long long CH = 1ll << 20;
+        for (long long p0 = 0; p0 < p; p0 += CH) {
+            PairMidArgs m;
+            const long long pn = p - p0 < CH ? p - p0 : CH;
+            m.x = (const bf16_t*)x + p0 * 128; m.w3 = (const bf16_t*)w3; m.s3 = scale3; m.h3 = shift3;
+            m.res = (const bf16_t*)residual + p0 * 512; m.w1 = (const bf16_t*)w1; m.s1 = scale1; m.h1 = shift1;
+            m.y = (bf16_t*)y + p0 * 512; m.z = (bf16_t*)z + p0 * 128; m.P = pn;
+            m.act3 = act3; m.act1 = act1; m.slope3 = slope3; m.slope1 = slope1;
+            const long long ntiles = (pn + 63) / 64;
+            const int grid = (int)(ntiles < g_pair_cus ? ntiles : g_pair_cus);
+            if (dtype == RR_F16) hipLaunchKernelGGL(k_pair_mid<f16_t>, dim3(grid), dim3(512), 0, s, m);
+            else hipLaunchKernelGGL(k_pair_mid<bf16_t>, dim3(grid), dim3(512), 0, s, m);
+        }
+        return check_launch("rr_conv1x1_pair");
+    }
     PairArgs a;
     a.x = (const bf16_t*)x; a.w3 = (const bf16_t*)w3; a.s3 = scale3; a.h3 = shift3; a.res = (const bf16_t*)residual;
     a.w1 = (const bf16_t*)w1; a.s1 = scale1; a.h1 = shift1; a.y = (bf16_t*)y; a.z = (bf16_t*)z; a.P = p;
@@ -511,7 +763,6 @@ extern "C" int rr_conv1x1_pair(const void* x, long long p, int c_in, const void*
     long long grid = (nstrips + 7) / 8;
     if (grid > g_pair_cus) grid = g_pair_cus;
     const dim3 g((unsigned)grid), b(512);
-    hipStream_t s = as_stream(stream);
     auto go = [&](auto h) {
         using H = decltype(h);
         if (c_out == 64 && !proj) hipLaunchKernelGGL((k_stream_pair<64, 2, false, H>), g, b, 0, s, a);

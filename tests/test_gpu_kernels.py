@@ -130,6 +130,23 @@ def test_conv3x3_direct(cuda, case, mode, prec):
         E.lib().rr_set_tuning(6, 1)
 
 
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_conv3x3_pipelined_schedule_bit_identical(cuda, prec):
+    """RR_TUNE_CONV3_PIPE: the software-pipelined A-stationary tile loop issues
+    the same MFMAs in the same accumulation order as the compiler-scheduled one,
+    so the outputs are bit-identical (and both match the float64 reference)."""
+    from cirtorch import _engine as E
+    case = (3, 64, 24, 96, 64, 3, 1, 1, False, True)
+    outs = []
+    try:
+        for pipe in (0, 1):
+            E.check(E.lib().rr_set_tuning(10, pipe), "rr_set_tuning")
+            outs.append(_check_conv(cuda, case, prec, True))
+    finally:
+        E.lib().rr_set_tuning(10, 1)
+    assert torch.equal(outs[0], outs[1])
+
+
 def _check_conv(cuda, case, prec, perm):
     n, cin, h, w, cout, k, s, p, use_res, leaky = case
     g = torch.Generator().manual_seed(hash(case) & 0xFFFF)
@@ -178,6 +195,7 @@ def _check_conv(cuda, case, prec, perm):
     # fp16 output rounding: 2^-11 relative
     tol = 2e-5 * scale_ref if prec == "fp32" else (8e-3 if prec == "bf16" else 2e-3) * scale_ref
     assert err <= tol, (err, scale_ref)
+    return y
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
@@ -332,6 +350,62 @@ def test_conv1x1_pair(cuda, dt, c_out, shape):
     z2 = ops.conv2d_fused(y2, w1p, 1, 1, 1, 0, c_out, c[2], c[3], leaky=True, perm32=True)
     assert torch.equal(y.cpu(), y2.cpu())
     assert (z.float() == z2.float()).float().mean().item() > 0.99
+
+
+def _mod3_pair_case(dt, n, h, w, seed, cuda, ref=True):
+    rnd = lambda t: t.to(dt).float()  # noqa: E731
+    g = torch.Generator().manual_seed(seed)
+    ops = _ops()
+    x = rnd(torch.randn(n, 128, h, w, generator=g))
+    w3 = rnd(torch.randn(512, 128, 1, 1, generator=g) * (2.0 / 128) ** 0.5)
+    w1 = rnd(torch.randn(128, 512, 1, 1, generator=g) * (2.0 / 512) ** 0.5)
+    s3, h3 = torch.rand(512, generator=g) + 0.5, torch.randn(512, generator=g) * 0.1
+    s1, h1 = torch.rand(128, generator=g) + 0.5, torch.randn(128, generator=g) * 0.1
+    res = rnd(torch.randn(n, 512, h, w, generator=g))
+    xe = x.permute(0, 2, 3, 1).contiguous().to(dt).to(cuda)
+    re = res.permute(0, 2, 3, 1).contiguous().to(dt).to(cuda)
+    w3p = ops.pack_conv_weights(w3.to(cuda), 128, dt, perm32=True)
+    w1p = ops.pack_conv_weights(w1.to(cuda), 512, dt, perm32=True)
+    c = [t.to(cuda) for t in (s3, h3, s1, h1)]
+    y, z = ops.conv1x1_pair(xe, w3p, c[0], c[1], re, True, 0.01, w1p, c[2], c[3], 128, True, 0.01)
+    if ref:
+        yr = F.leaky_relu(F.conv2d(x.double(), w3.double()) * s3.double()[None, :, None, None]
+                          + h3.double()[None, :, None, None] + res.double(), 0.01)
+        zr = F.leaky_relu(F.conv2d(rnd(yr.float()).double(), w1.double()) * s1.double()[None, :, None, None]
+                          + h1.double()[None, :, None, None], 0.01)
+        gy = y.float().permute(0, 3, 1, 2).cpu().double()
+        gz = z.float().permute(0, 3, 1, 2).cpu().double()
+        assert (gy - yr).abs().max().item() <= 8e-3 * yr.abs().max().item()
+        assert (gz - zr).abs().max().item() <= 1.6e-2 * zr.abs().max().item()
+    # the two unfused launches on the same inputs
+    y2 = ops.conv2d_fused(xe, w3p, 1, 1, 1, 0, 512, c[0], c[1], residual=re, leaky=True, perm32=True)
+    z2 = ops.conv2d_fused(y2, w1p, 1, 1, 1, 0, 128, c[2], c[3], leaky=True, perm32=True)
+    return y, z, y2, z2
+
+
+@pytest.mark.parametrize("shape", [(2, 23, 37), (1, 37, 113), (4, 48, 64)])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_conv1x1_pair_mod3(cuda, dt, shape):
+    """The 128 -> 512 -> 128 boundary (k_pair_mid: weights in VGPRs, LDS-DMA
+    tiles of 64 pixels, partial last tile) vs a float64 restatement and vs the
+    two unfused launches: y bit-identical, z bit-identical where the unfused
+    conv1 is the streaming kernel (same K-step order), else >= 99 %."""
+    n, h, w = shape
+    y, z, y2, z2 = _mod3_pair_case(dt, n, h, w, 11 * h + w, cuda)
+    assert torch.equal(y.cpu(), y2.cpu())
+    if n * h * w >= 4096:
+        assert torch.equal(z.cpu(), z2.cpu())
+    else:
+        assert (z.float() == z2.float()).float().mean().item() > 0.99
+
+
+def test_conv1x1_pair_mod3_pixel_chunks(cuda):
+    """More than 2^20 pixels: the C-ABI runs the boundary in 2^20-pixel chunks
+    (32-bit buffer offsets); every chunk bit-identical to the unfused launches."""
+    y, z, y2, z2 = _mod3_pair_case(torch.bfloat16, 1, 1031, 1029, 5, cuda, ref=False)
+    assert y.shape[1] * y.shape[2] > (1 << 20)
+    assert torch.equal(y, y2)
+    assert torch.equal(z, z2)
 
 
 @pytest.mark.parametrize("c_out", [64, 128])

@@ -177,3 +177,22 @@ def test_extract_vectors_iss_test_transform(cuda, tmp_path):
     assert torch.equal(a, b_)
     assert tuple(imgs[0].shape[1:]) == tf.output_size(210, 150)[::-1] == (91, 128)
     assert tuple(imgs[1].shape[1:]) == tf.output_size(175, 130)[::-1]
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_backbone_mod3_boundary_fusion_bit_identical(cuda, prec, monkeypatch):
+    """ResNet-50 body with the 128/512 boundaries fused (k_pair_mid, default)
+    vs the same body with them as two launches (RR_PAIR_MID=0): every stage
+    output bit-identical (same MFMA K-step order and roundings)."""
+    from cirtorch.backbones import resnet
+    from cirtorch.models.init import random_init_
+    body = resnet.resnet50(precision=prec)
+    random_init_(body, 3)
+    body = body.to(cuda).eval()
+    x = torch.rand(2, 3, 256, 512, generator=torch.Generator().manual_seed(4)).to(cuda)
+    with torch.no_grad():
+        fused = body(x)
+        monkeypatch.setenv("RR_PAIR_MID", "0")
+        plain = body(x)
+    for k in fused:
+        assert torch.equal(fused[k], plain[k]), k
