@@ -71,6 +71,7 @@ def parse():
     ap.add_argument("--c3-batch", type=int, default=16, help="config 3: images per multi-scale R101 step")
     ap.add_argument("--c5-batch", type=int, default=64, help="config 5: images per R152 fp16 step")
     ap.add_argument("--c5-db-rows", type=int, default=10_000_000, help="config 5: fp16 database rows (0 = skip)")
+    ap.add_argument("--tune", default="", help="developer A/B: rr_set_tuning pairs key=value[,key=value]")
     return ap.parse_args()
 
 
@@ -463,9 +464,13 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from cirtorch import _ops
+    from cirtorch import _engine as E
     from cirtorch.models.GF_net import make_net
     from cirtorch.models.init import random_init_
     from cirtorch.search import ShardedIndex
+    for kv in filter(None, args.tune.split(",")):
+        k_, v_ = kv.split("=")
+        E.check(E.lib().rr_set_tuning(int(k_), int(v_)), "rr_set_tuning")
 
     net = make_net(args.arch, precision=args.precision, mean=[0.485, 0.456, 0.406], std=[0.229, 0.224, 0.225])
     random_init_(net, seed=0)

@@ -23,6 +23,8 @@
 // (the max-pool is exact on the same bf16 values).
 #include "rr_internal.h"
 
+#include <type_traits>
+
 namespace rr {
 
 namespace {
@@ -228,6 +230,248 @@ __global__ void __launch_bounds__(NT) k_stem_pool(StemArgs a, int tiles_w, int t
     }
 }
 
+// ---------------------------------------------------------------------------
+// Stem v2: pool BEFORE the epilogue.  f(v) = round16(act(|s| * v + h)) is
+// non-decreasing in v (fma with |s| >= 0, leaky with slope in [0, 1], RNE),
+// so max-pool(f(conv)) == f(max-pool(conv)) exactly.  Output channels whose
+// BN scale is negative get their weight rows negated when the fragments are
+// loaded (bf16/fp16 negation and the MFMA sum are sign-symmetric, so the
+// accumulator is exactly -conv) and use |s|: every value equals the select-
+// form result of k_stem_pool bit for bit, and BN + activation + packing run
+// on the 4x fewer pooled pixels only.
+// Work layout: a tile is PH = 8 pooled rows x PW = 56 pooled cols; wave w
+// owns stem columns 14w .. 14w + 15 (one 16-pixel B fragment per stem row,
+// 2 columns of overlap: 7 pooled columns) and walks the 17 stem rows top to
+// bottom: the vertical 3-max of each pooled row is a per-lane max3 over the
+// accumulators of 3 consecutive stem rows (kept in VGPRs), the horizontal
+// 3-max two DPP row shifts (lane i <- lanes i+1, i+2 of the 16-pixel row).
+// No LDS round trip and no barrier for the pooling; one barrier per tile for
+// the double-buffered input patch (normalised fp32 -> packed 16-bit,
+// [row][col][4 ch], 39 x 234 pixels).
+template <typename HT, bool U8>
+__global__ void __launch_bounds__(NT) k_stem_pool2(StemArgs a, int tiles_w, int tiles_hw, int ntiles) {
+    constexpr int PH = 8, PW = 56, SRN = 2 * PH + 1, CB = 14;
+    constexpr int IR = 2 * (SRN - 1) + 7;            // 39 input rows
+    constexpr int SCN = CB * 7 + 16;                 // 114 stem columns
+    constexpr int IC = 2 * (SCN - 1) + 8;            // 234 input columns (even: 16-B pixel pairs)
+    constexpr int HIC = IC / 2;
+    constexpr int NPAIR = IR * HIC, PPT = (NPAIR + NT - 1) / NT;
+    constexpr int PATCH = IR * IC * 8;
+    static_assert(PW == 7 * (NT / 64), "one 7-pooled-column block per wave");
+    __shared__ __attribute__((aligned(16))) char sP[2][PATCH];
+    __shared__ __attribute__((aligned(16))) float sS[64], sH[64];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r16 = lane & 15, q = lane >> 4;
+    const int H = a.h, W = a.w_;
+    const long long plane = (long long)H * W;
+
+    if (tid < 64) {
+        sS[tid] = fabsf(a.scale[tid]);
+        sH[tid] = a.shift[tid];
+    }
+    // weights -> VGPRs (fragment i = packed rows 16i .. 16i+15, K-step m = kernel row),
+    // rows of negative-scale channels negated (sign bit of every 16-bit element)
+    uint4 areg[4][7];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const unsigned flip = a.scale[perm32_channel(i * 16 + r16)] < 0.f ? 0x80008000u : 0u;
+#pragma unroll
+        for (int m = 0; m < 7; ++m) {
+            uint4 w = a.w[(i * 16 + r16) * 32 + m * 4 + q];
+            w.x ^= flip; w.y ^= flip; w.z ^= flip; w.w ^= flip;
+            areg[i][m] = w;
+        }
+    }
+
+    auto tile_origin = [&](int t, int& img, int& ph0, int& pw0) {
+        img = t / tiles_hw;
+        const int rem = t - img * tiles_hw;
+        const int th = rem / tiles_w;
+        ph0 = th * PH;
+        pw0 = (rem - th * tiles_w) * PW;
+    };
+
+    // patch fill: pixel pairs (2 adjacent input columns) -> one 16-B LDS store;
+    // in two halves (pairs u < PH1, u >= PH1) so only half the raw pixels are
+    // live in VGPRs while the MFMAs run
+    constexpr int PH1 = (PPT + 1) / 2;
+    float pf[PH1][6];
+    auto fill_load = [&](int t, int half) {
+        int img, ph0, pw0;
+        tile_origin(t, img, ph0, pw0);
+        const int ir0 = 4 * ph0 - 5, ic0 = 4 * pw0 - 5;
+        // one raw buffer per image (3 planes) with 32-bit offsets; a pixel outside
+        // the image gets an offset past the buffer (reads 0) -- never a negative
+        // one -- and is zeroed after normalisation in fill_store anyway
+        constexpr int ESZ = U8 ? 1 : 4;
+        constexpr unsigned OOBO = 0x80000000u;
+        const char* ib = (const char*)a.x + (long long)img * 3 * plane * ESZ;
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc((void*)ib, (short)0, (int)(3 * plane * ESZ), 0x00020000);
+#pragma unroll
+        for (int uu = 0; uu < PH1; ++uu) {
+            const int u = half * PH1 + uu;
+            if (u >= PPT) break;
+            const int k = tid + NT * u;
+            const int kk = k < NPAIR ? k : NPAIR - 1;
+            const int r = kk / HIC, c = 2 * (kk - r * HIC);
+            const int ih = ir0 + r, iw = ic0 + c;
+            const bool rok = (unsigned)ih < (unsigned)H;
+            const int o = (ih * W + iw) * ESZ;
+            const unsigned off0 = rok && (unsigned)iw < (unsigned)W ? (unsigned)o : OOBO;
+            const unsigned off1 = rok && (unsigned)(iw + 1) < (unsigned)W ? (unsigned)(o + ESZ) : OOBO;
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) {
+                const unsigned po = (unsigned)(ch * (int)plane * ESZ);
+                if constexpr (U8) {  // IEEE division: the same float as torch's / numpy's x / 255
+                    pf[uu][2 * ch] = (float)__builtin_amdgcn_raw_buffer_load_b8(rs, (int)(off0 + po), 0, 0) / 255.f;
+                    pf[uu][2 * ch + 1] = (float)__builtin_amdgcn_raw_buffer_load_b8(rs, (int)(off1 + po), 0, 0) / 255.f;
+                } else {
+                    pf[uu][2 * ch] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(off0 + po), 0, 0));
+                    pf[uu][2 * ch + 1] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(off1 + po), 0, 0));
+                }
+            }
+        }
+    };
+    auto fill_store = [&](int t, int buf, int half) {
+        int img, ph0, pw0;
+        tile_origin(t, img, ph0, pw0);
+        const int ir0 = 4 * ph0 - 5, ic0 = 4 * pw0 - 5;
+#pragma unroll
+        for (int uu = 0; uu < PH1; ++uu) {
+            const int u = half * PH1 + uu;
+            if (u >= PPT) break;
+            const int k = tid + NT * u;
+            if (k >= NPAIR) continue;
+            const int r = k / HIC, c = 2 * (k - r * HIC);
+            const bool rok = (unsigned)(ir0 + r) < (unsigned)H;
+            const bool ok0 = rok && (unsigned)(ic0 + c) < (unsigned)W;
+            const bool ok1 = rok && (unsigned)(ic0 + c + 1) < (unsigned)W;
+            float v[6];
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) {  // zero padding is applied AFTER normalisation
+                const float x0 = pf[uu][2 * ch], x1 = pf[uu][2 * ch + 1];
+                v[2 * ch] = ok0 ? (a.do_norm ? (x0 - a.mean[ch]) * a.rstd[ch] : x0) : 0.f;
+                v[2 * ch + 1] = ok1 ? (a.do_norm ? (x1 - a.mean[ch]) * a.rstd[ch] : x1) : 0.f;
+            }
+            uint4 o;
+            o.x = H16<HT>::pack2(v[0], v[2]);
+            o.y = H16<HT>::pack2(v[4], 0.f);
+            o.z = H16<HT>::pack2(v[1], v[3]);
+            o.w = H16<HT>::pack2(v[5], 0.f);
+            *reinterpret_cast<uint4*>(sP[buf] + (r * IC + c) * 8) = o;
+        }
+    };
+
+    const float slope = a.leaky ? a.slope : 1.f;  // identity == leaky with slope 1
+    const float NINF = -__builtin_inff();
+    int t = blockIdx.x;
+    if (t >= ntiles) return;
+    fill_load(t, 0);
+    fill_store(t, 0, 0);
+    fill_load(t, 1);
+    fill_store(t, 0, 1);
+    __syncthreads();
+    int cur = 0;
+    for (; t < ntiles; t += gridDim.x, cur ^= 1) {
+        const int tn = t + gridDim.x;
+        if (tn < ntiles) fill_load(tn, 0);
+        int img, ph0, pw0;
+        tile_origin(t, img, ph0, pw0);
+        const int cb = CB * wave;
+        const char* pb = sP[cur] + (2 * (cb + r16) + 2 * q) * 8;
+        // this wave's pooled columns: skip the wave when all of them lie past the map
+        const bool active = pw0 + 7 * wave < a.wp;
+        // even stem dims (host-checked): the only stem pixels outside the map that
+        // feed stored outputs are row -1 (top tiles) and column -1 (left tiles,
+        // wave 0, lane 0)
+        const bool left = pw0 == 0 && wave == 0;
+        auto pool_out = [&](int pr, const h16_f32x4_t (&m)[4]) {
+            float hv[4][4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float v = m[i][e];
+                    const float v1 = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x101, 0xF, 0xF, false));
+                    const float v2 = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x102, 0xF, 0xF, false));
+                    hv[i][e] = fmaxf(fmaxf(v, v1), v2);
+                }
+            const int pc = 7 * wave + (r16 >> 1);
+            if ((r16 & 1) == 0 && r16 < 14 && ph0 + pr < a.hp && pw0 + pc < a.wp) {
+                bf16_t* dst = a.y + (((long long)img * a.hp + ph0 + pr) * a.wp + pw0 + pc) * 64;
+#pragma unroll
+                for (int i2 = 0; i2 < 2; ++i2) {
+                    const int cl = 32 * i2 + 8 * q;  // 8 consecutive channels (PERM32 rows)
+                    float v[8];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        v[r] = hv[2 * i2][r] * sS[cl + r] + sH[cl + r];
+                        v[4 + r] = hv[2 * i2 + 1][r] * sS[cl + 4 + r] + sH[cl + 4 + r];
+                    }
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) v[r] = fmaxf(v[r], v[r] * slope);
+                    uint4 o;
+                    o.x = H16<HT>::pack2(v[0], v[1]);
+                    o.y = H16<HT>::pack2(v[2], v[3]);
+                    o.z = H16<HT>::pack2(v[4], v[5]);
+                    o.w = H16<HT>::pack2(v[6], v[7]);
+                    *reinterpret_cast<uint4*>(dst + cl) = o;
+                }
+            }
+        };
+        auto stem_row = [&](int r, h16_f32x4_t (&acc)[4]) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[i] = (h16_f32x4_t){0.f, 0.f, 0.f, 0.f};
+            const char* rb = pb + r * (2 * IC * 8);
+#pragma unroll
+            for (int m = 0; m < 7; ++m) {
+                const uint4 b = *reinterpret_cast<const uint4*>(rb + m * IC * 8);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc[i] = H16<HT>::mfma(areg[i][m], b, acc[i]);
+            }
+        };
+        h16_f32x4_t A[4];
+        if (active) {
+            stem_row(0, A);
+            if (ph0 == 0) {  // stem row -1: max-pool padding
+#pragma unroll
+                for (int i = 0; i < 4; ++i) A[i] = (h16_f32x4_t){NINF, NINF, NINF, NINF};
+            }
+        }
+        for (int pr = 0; pr < PH; ++pr) {
+            if (pr == PH / 2 && tn < ntiles) {  // first half of the next patch -> LDS, second half in flight
+                fill_store(tn, cur ^ 1, 0);
+                fill_load(tn, 1);
+            }
+            if (active) {
+                h16_f32x4_t B[4], C[4], m3[4];
+                stem_row(2 * pr + 1, B);
+                stem_row(2 * pr + 2, C);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) m3[i][e] = fmaxf(fmaxf(A[i][e], B[i][e]), C[i][e]);
+                if (left) {  // stem column -1 (lane 0 of wave 0): max-pool padding; the DPP
+                             // shifts in pool_out then run with every lane active
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) m3[i][e] = r16 == 0 ? NINF : m3[i][e];
+                }
+                pool_out(pr, m3);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) A[i] = C[i];
+            }
+        }
+        if (tn < ntiles) fill_store(tn, cur ^ 1, 1);
+        __syncthreads();
+    }
+}
+
+
 // out[R][k], R packed row (PERM32), k = kh*32 + kw*4 + ci (kh < 7, kw < 7, ci < 3 real; rest 0)
 template <typename HT>
 __global__ void k_stem_pack(const float* __restrict__ w, HT* __restrict__ out) {
@@ -261,6 +505,10 @@ extern "C" int rr_stem_pack_weights(const float* w, int c_out, int c_in, int kh,
     return check_launch("rr_stem_pack_weights");
 }
 
+namespace rr {
+int g_stem_mode = 1;  // rr_set_tuning(RR_TUNE_STEM): 1 pool-before-epilogue kernel (v2), 0 k_stem_pool
+}
+
 template <bool U8>
 static int stem_conv_pool(const void* x, int n, int h, int w, const float* mean_host, const float* std_host,
                           int do_normalize, const void* wpk, const float* scale, const float* shift, int act,
@@ -289,11 +537,25 @@ static int stem_conv_pool(const void* x, int n, int h, int w, const float* mean_
     a.leaky = act == RR_ACT_LEAKY;
     if (a.leaky && !(slope >= 0.f && slope <= 1.f)) return fail(RR_EINVAL, "rr_stem_conv_pool: leaky slope must be in [0, 1]");
     a.slope = slope;
+    const int g_stem_cus = grid_cus();
+    if (g_stem_mode == 1 && ho % 2 == 0 && wo % 2 == 0) {  // v2 handles the even stem maps (borders top / left)
+        constexpr int PH = 8, PW = 56;
+        const int tiles_w = (wp + PW - 1) / PW, tiles_h = (hp + PH - 1) / PH;
+        const long long ntiles = (long long)n * tiles_h * tiles_w;
+        if (ntiles >= (1ll << 31)) return fail(RR_EINVAL, "rr_stem_conv_pool: too many tiles");
+        const int grid = (int)(ntiles < g_stem_cus ? ntiles : g_stem_cus);
+        if (dtype == RR_F16)
+            hipLaunchKernelGGL((k_stem_pool2<f16_t, U8>), dim3(grid), dim3(NT), 0, as_stream(stream), a, tiles_w,
+                               tiles_w * tiles_h, (int)ntiles);
+        else
+            hipLaunchKernelGGL((k_stem_pool2<bf16_t, U8>), dim3(grid), dim3(NT), 0, as_stream(stream), a, tiles_w,
+                               tiles_w * tiles_h, (int)ntiles);
+        return check_launch("rr_stem_conv_pool");
+    }
     constexpr int PH = 4, PW = 32;
     const int tiles_w = (wp + PW - 1) / PW, tiles_h = (hp + PH - 1) / PH;
     const long long ntiles = (long long)n * tiles_h * tiles_w;
     if (ntiles >= (1ll << 31)) return fail(RR_EINVAL, "rr_stem_conv_pool: too many tiles");
-    const int g_stem_cus = grid_cus();
     const int grid = (int)(ntiles < g_stem_cus ? ntiles : g_stem_cus);
     if (dtype == RR_F16)
         hipLaunchKernelGGL((k_stem_pool<PH, PW, f16_t, U8>), dim3(grid), dim3(NT), 0, as_stream(stream), a, tiles_w,

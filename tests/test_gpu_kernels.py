@@ -310,6 +310,46 @@ def test_stem_conv_pool(cuda, dt, shape, norm):
     assert (got == un).float().mean().item() > 0.95
 
 
+@pytest.mark.parametrize("shape", [(2, 61, 83), (1, 96, 470), (3, 200, 130)])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_stem_pool_before_epilogue_bit_identical(cuda, dt, shape):
+    """RR_TUNE_STEM: the v2 stem pools the raw conv and applies BN + leaky +
+    rounding to the pooled pixels only (exact: the epilogue is non-decreasing
+    once negative-scale rows are negated).  Positive- and zero-scale channels
+    are bit-identical to the v1 kernel; negative-scale channels differ only
+    where the MFMA sum of the negated products is not the exact negation of
+    the original sum (1 ulp of the f32 accumulator: measured 2 of 180k fp16
+    outputs, 1 output ulp), fp32 and uint8 inputs."""
+    n, h, w = shape
+    g = torch.Generator().manual_seed(h + 7 * w)
+    x = torch.rand(n, 3, h, w, generator=g)
+    wt = torch.randn(64, 3, 7, 7, generator=g) * 0.1
+    scale = torch.rand(64, generator=g) + 0.5
+    scale[::3] *= -1.0
+    scale[5] = 0.0
+    shift = torch.randn(64, generator=g) * 0.1
+    mean, std = [0.485, 0.456, 0.406], [0.229, 0.224, 0.225]
+    ops = _ops()
+    from cirtorch import _engine as E
+    wpk = ops.pack_stem_weights(wt.to(cuda), dt)
+    xu = (x * 255).to(torch.uint8)
+    outs = {}
+    try:
+        for mode in (0, 1):
+            E.check(E.lib().rr_set_tuning(11, mode), "rr_set_tuning")
+            outs[mode] = [ops.stem_conv_pool(inp.to(cuda), wpk, scale.to(cuda), shift.to(cuda), leaky=True,
+                                             slope=0.01, mean=mean, std=std).float().cpu() for inp in (x, xu)]
+    finally:
+        E.lib().rr_set_tuning(11, 1)
+    neg = scale < 0
+    ulp = 2.0 ** -7 if dt == torch.bfloat16 else 2.0 ** -10
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a[..., ~neg], b[..., ~neg])
+        d = (a[..., neg] - b[..., neg]).abs()
+        assert (d > 0).float().mean().item() < 1e-3
+        assert (d <= ulp * a[..., neg].abs().clamp_min(1.0)).all()
+
+
 @pytest.mark.parametrize("c_out", [64, 128])
 @pytest.mark.parametrize("shape", [(2, 23, 37), (1, 64, 96)])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])

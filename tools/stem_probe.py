@@ -10,7 +10,15 @@ import torch  # noqa: E402
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tune", default="", help="rr_set_tuning pairs key=value[,key=value]")
+    args = ap.parse_args()
     from cirtorch import _ops
+    from cirtorch import _engine as E
+    for kv in filter(None, args.tune.split(",")):
+        k_, v_ = kv.split("=")
+        E.check(E.lib().rr_set_tuning(int(k_), int(v_)), "rr_set_tuning")
     x = torch.rand(32, 3, 768, 1024, device="cuda")
     w = torch.randn(64, 3, 7, 7, device="cuda") * 0.1
     wp = _ops.pack_stem_weights(w)
