@@ -71,6 +71,11 @@ def parse():
     ap.add_argument("--c3-batch", type=int, default=16, help="config 3: images per multi-scale R101 step")
     ap.add_argument("--c5-batch", type=int, default=64, help="config 5: images per R152 fp16 step")
     ap.add_argument("--c5-db-rows", type=int, default=10_000_000, help="config 5: fp16 database rows (0 = skip)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N > 1 process group: nccl (= RCCL over xGMI, the measured path) or gloo (host-copy "
+                         "rehearsal of the same code path)")
+    ap.add_argument("--one-device", action="store_true",
+                    help="rehearsal on a 1-GPU box: every rank on cuda:0 (with --dist-backend gloo)")
     ap.add_argument("--tune", default="", help="developer A/B: rr_set_tuning pairs key=value[,key=value]")
     return ap.parse_args()
 
@@ -457,17 +462,28 @@ def main():
     args = parse()
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
-    local = int(os.environ.get("LOCAL_RANK", 0))
+    local = 0 if args.one_device else int(os.environ.get("LOCAL_RANK", 0))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+
+    def max_over_ranks(x):
+        """max of a host float over the ranks (RCCL: a device tensor; gloo: a host one)"""
+        if world == 1:
+            return x
+        t = torch.tensor([x], device=dev if args.dist_backend == "nccl" else "cpu", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
 
     from cirtorch import _ops
     from cirtorch import _engine as E
     from cirtorch.models.GF_net import make_net
     from cirtorch.models.init import random_init_
-    from cirtorch.search import ShardedIndex
+    from cirtorch.search import ShardedIndex, all_gather_stacked
     for kv in filter(None, args.tune.split(",")):
         k_, v_ = kv.split("=")
         E.check(E.lib().rr_set_tuning(int(k_), int(v_)), "rr_set_tuning")
@@ -493,9 +509,7 @@ def main():
     def match(desc):
         q = desc.t().contiguous()
         if world > 1:
-            qa = torch.empty((world * B, q.shape[1]), dtype=q.dtype, device=dev)
-            dist.all_gather_into_tensor(qa, q)
-            q = qa
+            q = all_gather_stacked(q).reshape(world * B, q.shape[1])
         return index.search(q, args.k)
 
     EB = max(1, min(args.extract_batch, B))
@@ -539,11 +553,7 @@ def main():
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
-        elapsed = time.perf_counter() - t0
-        if world > 1:
-            t = torch.tensor([elapsed], device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            elapsed = float(t.item())
+        elapsed = max_over_ranks(time.perf_counter() - t0)
         body_ms = sum(a.elapsed_time(b) for a, b in ev_pairs) / args.steps   # extractor time per step
 
         # extract-only loop (same net, no matching)
@@ -552,7 +562,7 @@ def main():
         for _ in range(max(3, args.steps // 2)):
             extract_all(False)
         torch.cuda.synchronize()
-        ext_only = max(3, args.steps // 2) * B / (time.perf_counter() - t1)
+        ext_only = max(3, args.steps // 2) * B / max_over_ranks(time.perf_counter() - t1)
 
         # PCIe-inclusive extraction (not `value`: the timed step starts with the
         # images resident in HBM): the step's B images from pinned host memory,
@@ -622,11 +632,7 @@ def main():
             torch.cuda.synchronize()
             if world > 1:
                 dist.barrier()
-            tk = (time.perf_counter() - t2) / args.knn_steps
-            if world > 1:
-                t = torch.tensor([tk], device=dev)
-                dist.all_reduce(t, op=dist.ReduceOp.MAX)
-                tk = float(t.item())
+            tk = max_over_ranks((time.perf_counter() - t2) / args.knn_steps)
             flops = 2.0 * args.knn_q * n_local * args.dim
             peak = PEAK_F32_TFLOPS if args.precision == "fp32" else PEAK_BF16_TFLOPS
             knn = {"queries_per_sec": args.knn_q / tk, "q": args.knn_q, "db_rows": args.db_rows, "k": args.k,
