@@ -210,6 +210,20 @@ def _decode(item, image_size, bbx, transform, tf):
     return transform(pil) if transform is not None else _to_pixels(pil)
 
 
+_PINNED = [None, None]  # one grown-on-demand pinned staging buffer per double-buffer slot, kept across calls
+
+
+def _pinned_chain(slot, shape, dtype):
+    """pinned host view of `shape` in slot's staging buffer: pinning 150 MB
+    per chain costs more than the chain's H2D, so the buffer is reused (the
+    caller has waited for the slot's previous copy)."""
+    n = int(np.prod(shape)) * torch.empty((), dtype=dtype).element_size()
+    buf = _PINNED[slot]
+    if buf is None or buf.numel() < n:
+        buf = _PINNED[slot] = torch.empty(n, dtype=torch.uint8).pin_memory()
+    return buf[:n].view(dtype).view(shape)
+
+
 def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], msp=1, print_freq=10,
                     batch=64, workers=8, test_transform=None):
     """Upstream ``extract_vectors`` (``scripts/test.py:200,236-238``): returns a
@@ -238,7 +252,6 @@ def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], 
     ms = list(ms)
     main = torch.cuda.current_stream(dev)
     copy = torch.cuda.Stream(dev)
-    pinned = {}
     copied = [torch.cuda.Event(), torch.cuda.Event()]
     freed = [torch.cuda.Event(), torch.cuda.Event()]
     for e in freed:
@@ -251,12 +264,11 @@ def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], 
         """one same-size group of images -> their descriptor columns"""
         slot = state["slot"]
         if len(part) > 1:
-            key = (slot, len(part), tuple(items[0].shape), items[0].dtype)
-            host = pinned.get(key)
-            if host is None:
-                host = pinned[key] = torch.empty((len(part),) + tuple(items[0].shape), dtype=items[0].dtype).pin_memory()
-            copied[slot].synchronize()        # the previous H2D out of this host buffer has finished
-            torch.stack(items, out=host)
+            copied[slot].synchronize()        # the previous H2D out of this slot's host buffer has finished
+            host = _pinned_chain(slot, (len(part),) + tuple(items[0].shape), items[0].dtype)
+            # gather into the pinned chain on several host threads (torch copies
+            # release the GIL): one thread's memcpy rate would bound the chain
+            list(state["gather"].map(lambda j: host[j].copy_(items[j]), range(len(part))))
         else:
             host = items[0][None]
         copy.wait_event(freed[slot])          # the extractor is done with this slot's device buffer
@@ -292,7 +304,9 @@ def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], 
         net.augment = None
     win = max(1, 8 * batch)
     try:
-        with ThreadPoolExecutor(max_workers=max(1, workers)) as pool, torch.no_grad():
+        with ThreadPoolExecutor(max_workers=max(1, workers)) as pool, \
+                ThreadPoolExecutor(max_workers=8) as gather, torch.no_grad():
+            state["gather"] = gather
             def submit(w0):
                 return [pool.submit(_decode, images[i], image_size, bbxs[i] if bbxs is not None else None,
                                     transform, test_transform) for i in range(w0, min(n, w0 + win))]

@@ -39,7 +39,7 @@ __device__ __forceinline__ int wswz(int row, int chunk) {
 }
 
 template <int TC, int K, int FN, int D, int NW, bool RES, typename H>
-__global__ void __launch_bounds__(64 * NW) k_stream1x1(ConvArgs a, int nslices) {
+__global__ void __launch_bounds__(64 * NW) k_stream1x1(ConvArgs a, int nslices, int xmap) {
     constexpr int NI = TC / 16;   // accumulator fragments (channels) per wave
     constexpr int NK = K / 32;    // MFMA K-steps
     constexpr int NR = TC / 32;   // 16-B epilogue vectors per pixel
@@ -50,8 +50,14 @@ __global__ void __launch_bounds__(64 * NW) k_stream1x1(ConvArgs a, int nslices) 
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int slice = (int)blockIdx.x % nslices;
-    const int bi = (int)blockIdx.x / nslices;
+    // xmap (grid a multiple of 8 x nslices): blocks b, b + 8, b + 16, ... share
+    // an XCD (workgroups go round-robin over the 8 XCDs), so the nslices blocks
+    // that stream the same strips for different channel slices are put there:
+    // a strip's input is fetched into one XCD's L2 and re-read from it, not
+    // fetched by nslices XCDs from HBM
+    const int b = (int)blockIdx.x;
+    const int slice = xmap ? (b >> 3) % nslices : b % nslices;
+    const int bi = xmap ? ((b >> 3) / nslices) * 8 + (b & 7) : b / nslices;
     const int G = (int)gridDim.x / nslices;
     const int c0 = slice * TC;
 
@@ -644,6 +650,10 @@ __global__ void __launch_bounds__(512, 1) k_pair_mid(PairMidArgs a) {
 }
 
 
+}  // namespace
+int g_stream_xcd = 1;  // rr_set_tuning(RR_TUNE_STREAM_XCD): channel slices of one strip on one XCD
+namespace {
+
 template <int TC, int K, int FN, int D, int NW, typename H>
 void launch_s_t(const ConvArgs& a, hipStream_t s) {
     const int g_stream_cus = grid_cus();
@@ -656,10 +666,11 @@ void launch_s_t(const ConvArgs& a, hipStream_t s) {
     const long long need = (nstrips + NW - 1) / NW;
     if (per_slice > need) per_slice = need;
     const int grid = (int)(per_slice * nslices);
+    const int xmap = g_stream_xcd && nslices > 1 && grid % (8 * nslices) == 0;
     if (a.flags & RR_CONV_RESIDUAL)
-        hipLaunchKernelGGL((k_stream1x1<TC, K, FN, D, NW, true, H>), dim3(grid), dim3(64 * NW), 0, s, a, nslices);
+        hipLaunchKernelGGL((k_stream1x1<TC, K, FN, D, NW, true, H>), dim3(grid), dim3(64 * NW), 0, s, a, nslices, xmap);
     else
-        hipLaunchKernelGGL((k_stream1x1<TC, K, FN, D, NW, false, H>), dim3(grid), dim3(64 * NW), 0, s, a, nslices);
+        hipLaunchKernelGGL((k_stream1x1<TC, K, FN, D, NW, false, H>), dim3(grid), dim3(64 * NW), 0, s, a, nslices, xmap);
 }
 
 }  // namespace

@@ -105,6 +105,29 @@ def test_conv_stream1x1(cuda, case, mode, prec):
         E.lib().rr_set_tuning(5, 1)
 
 
+XCD_CASES = [
+    # chip-filling streaming 1x1s whose grid is a multiple of 8 x slices (XCD map on)
+    (4, 256, 48, 64, 1024, 1, 1, 0, True, True),    # mod4 conv3: 4 slices of 256 channels
+    (2, 128, 96, 128, 512, 1, 1, 0, True, True),    # mod3 conv3: 2 slices
+    (2, 512, 48, 64, 2048, 1, 1, 0, True, True),    # mod5 conv3 shape: 16 slices of 128
+]
+
+
+@pytest.mark.parametrize("case", XCD_CASES)
+def test_stream1x1_xcd_map(cuda, case):
+    """RR_TUNE_STREAM_XCD: the channel-slice blocks of one strip on one XCD is a
+    pure block-to-work remapping: exact vs float64, bit-identical to the plain order."""
+    from cirtorch import _engine as E
+    outs = []
+    try:
+        for xcd in (1, 0):
+            E.check(E.lib().rr_set_tuning(12, xcd), "rr_set_tuning")
+            outs.append(_check_conv(cuda, case, "bf16", True))
+    finally:
+        E.lib().rr_set_tuning(12, 1)
+    assert torch.equal(outs[0], outs[1])
+
+
 CONV3_CASES = [
     # bf16 stride-1 3x3 shapes the direct LDS-patch kernel (rr_conv3.hip) takes
     (2, 64, 16, 64, 64, 3, 1, 1, False, True),     # c_in = c_out = 64: weights resident in LDS
