@@ -61,6 +61,11 @@ _SIGS = {
     "rr_knn_topk": ([_vp, _vp, _ll, _vp, _vp, _i, _i, _i, _i, _ll, _vp, _vp, _vp, _sz, _i, _vp], _i),
     "rr_knn_topk_checked": ([_vp, _vp, _ll, _vp, _vp, _i, _i, _i, _i, _ll, _vp, _vp, _vp, _sz, _i, _f, _vp, _vp], _i),
     "rr_topk_merge": ([_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp], _i),
+    "rr_comm_unique_id": ([_vp, _i], _i),
+    "rr_comm_init": ([ctypes.POINTER(_vp), _i, _vp, _i, _i], _i),
+    "rr_comm_destroy": ([_vp], _i),
+    "rr_topk_allgather_workspace_bytes": ([_i, _i, _i], _sz),
+    "rr_topk_allgather_merge": ([_vp, _vp, _vp, _i, _i, _vp, _vp, _vp, _sz, _vp], _i),
     "rr_local_head_workspace_bytes": ([_ll, _i, _i], _sz),
     "rr_local_head": ([_vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _vp, _i, _vp, _vp, _sz, _vp], _i),
     "rr_mutual_nn": ([_vp, _i, _vp, _i, _vp, _vp], _i),

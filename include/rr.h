@@ -219,6 +219,24 @@ int rr_knn_topk_checked(const void* db, const float* db_f32, long long n_db,
 int rr_topk_merge(const double* in_scores, const long long* in_idx, int r, int nq, int k_in,
                   int k, double* out_scores, long long* out_idx, void* stream);
 
+/* ------------------------------------------------------ sharded search (RCCL) */
+/* For a non-Python host of the sharded search (one process per GPU; the Python
+ * host uses torch.distributed, cirtorch/search.py ShardedIndex).  RCCL is
+ * dlopen'ed on first use.  Rank 0 creates the id, the host sends it to every
+ * rank out of band, each rank calls rr_comm_init with its GPU current.  Then
+ * per search: rr_knn_topk on the local rows (idx_offset = the shard's first
+ * global row) -> rr_topk_allgather_merge = RCCL all-gather of the [nq][k]
+ * (score f64, index i64) lists over xGMI + rr_topk_merge, bit-identical to a
+ * 1-GPU search of the whole database.  Replaces the missing per-rank gather
+ * of scripts/train_globalF.py:667-730. */
+int rr_comm_unique_id(void* id_out, int id_bytes);                 /* id_bytes >= 128 */
+int rr_comm_init(void** comm, int nranks, const void* id, int id_bytes, int rank);
+int rr_comm_destroy(void* comm);
+size_t rr_topk_allgather_workspace_bytes(int nranks, int nq, int k);
+int rr_topk_allgather_merge(void* comm, const double* scores, const long long* idx, int nq, int k,
+                            double* out_scores, long long* out_idx, void* workspace, size_t workspace_bytes,
+                            void* stream);
+
 /* ------------------------------------------------------- local descriptors */
 /* Local-descriptor head (config 5): desc = normalize(W . grid_sample(x, kpts) + b).
  * Replaces cirtorch/modules/heads/local_head.py:43-71 (localHead.forward:

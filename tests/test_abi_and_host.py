@@ -188,3 +188,23 @@ def test_pmc_knn_traffic_profiles_match_bench_defaults():
         assert (c["q"], c["db_rows"], c["dim"], c["k"], c["screen"]) == (q, 1000000, 2048, 100, "bf16")
         # at least one pass over the bf16 database (4.096 GB)
         assert 4.0e9 < t["hbm_bytes_per_search"] < 2.0e10
+
+
+def test_comm_entry_points_validate_arguments():
+    """rr_comm_* / rr_topk_allgather_*: argument checks need no GPU (RCCL is
+    only dlopen'ed once a communicator is really created)."""
+    if not os.path.exists(LIB):
+        pytest.skip("librr.so not built")
+    import ctypes
+    from cirtorch import _engine
+    lib = _engine.lib()
+    comm = ctypes.c_void_p()
+    idbuf = ctypes.create_string_buffer(128)
+    assert lib.rr_comm_init(ctypes.byref(comm), 2, idbuf, 128, 2) != 0       # rank >= nranks
+    assert b"rank" in lib.rr_last_error()
+    assert lib.rr_comm_init(ctypes.byref(comm), 2, idbuf, 64, 0) != 0        # id shorter than ncclUniqueId
+    assert lib.rr_comm_unique_id(idbuf, 16) != 0
+    assert lib.rr_comm_destroy(None) == 0
+    assert lib.rr_topk_allgather_workspace_bytes(8, 1024, 100) >= 2 * 8 * 1024 * 100 * 8
+    assert lib.rr_topk_allgather_workspace_bytes(0, 1, 1) == 0
+    assert lib.rr_topk_allgather_merge(None, None, None, 1, 1, None, None, None, 0, None) != 0

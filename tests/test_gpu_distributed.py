@@ -74,3 +74,34 @@ def test_sharded_real_kernels_equal_single_search(cuda, world, n, prec):
         np.testing.assert_array_equal(s, s1)
     if n < k:
         assert (i1[:, n:] == -1).all()
+
+
+def test_c_abi_rccl_single_rank_merge(cuda):
+    """The C-ABI sharded-search exchange (rr_comm_* + rr_topk_allgather_merge,
+    RCCL dlopen'ed by librr.so) on a 1-rank communicator: the all-gather +
+    merge of one shard's top-k is that shard's top-k, bit for bit, and equals
+    the Python ShardedIndex path (world 1)."""
+    import ctypes
+    from cirtorch import _engine as E
+    from cirtorch.search import KnnIndex
+    from oracle import data
+    lib = E.lib()
+    db = torch.from_numpy(data.unit_rows(50000, 256, seed=61)).to(cuda)
+    q = torch.from_numpy(data.unit_rows(16, 256, seed=62)).to(cuda)
+    k = 20
+    s, i = KnnIndex(db, "bf16").search(q, k)
+    idbuf = ctypes.create_string_buffer(128)
+    E.check(lib.rr_comm_unique_id(idbuf, 128), "rr_comm_unique_id")
+    comm = ctypes.c_void_p()
+    E.check(lib.rr_comm_init(ctypes.byref(comm), 1, idbuf, 128, 0), "rr_comm_init")
+    try:
+        nbytes = lib.rr_topk_allgather_workspace_bytes(1, q.shape[0], k)
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=cuda)
+        os_ = torch.empty_like(s)
+        oi = torch.empty_like(i)
+        E.check(lib.rr_topk_allgather_merge(comm, E.ptr(s), E.ptr(i), q.shape[0], k, E.ptr(os_), E.ptr(oi),
+                                            E.ptr(ws), nbytes, E.stream_ptr(cuda)), "rr_topk_allgather_merge")
+        torch.cuda.synchronize()
+        assert torch.equal(oi, i) and torch.equal(os_, s)
+    finally:
+        E.check(lib.rr_comm_destroy(comm), "rr_comm_destroy")
