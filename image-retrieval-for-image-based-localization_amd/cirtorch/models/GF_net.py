@@ -266,9 +266,7 @@ def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], 
         if len(part) > 1:
             copied[slot].synchronize()        # the previous H2D out of this slot's host buffer has finished
             host = _pinned_chain(slot, (len(part),) + tuple(items[0].shape), items[0].dtype)
-            # gather into the pinned chain on several host threads (torch copies
-            # release the GIL): one thread's memcpy rate would bound the chain
-            list(state["gather"].map(lambda j: host[j].copy_(items[j]), range(len(part))))
+            torch.stack(items, out=host)      # (measured: faster than a per-image copy on 8 host threads)
         else:
             host = items[0][None]
         copy.wait_event(freed[slot])          # the extractor is done with this slot's device buffer
@@ -304,9 +302,7 @@ def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], 
         net.augment = None
     win = max(1, 8 * batch)
     try:
-        with ThreadPoolExecutor(max_workers=max(1, workers)) as pool, \
-                ThreadPoolExecutor(max_workers=8) as gather, torch.no_grad():
-            state["gather"] = gather
+        with ThreadPoolExecutor(max_workers=max(1, workers)) as pool, torch.no_grad():
             def submit(w0):
                 return [pool.submit(_decode, images[i], image_size, bbxs[i] if bbxs is not None else None,
                                     transform, test_transform) for i in range(w0, min(n, w0 + win))]
