@@ -76,6 +76,8 @@ def parse():
                          "rehearsal of the same code path)")
     ap.add_argument("--one-device", action="store_true",
                     help="rehearsal on a 1-GPU box: every rank on cuda:0 (with --dist-backend gloo)")
+    ap.add_argument("--extract-priority", type=int, default=int(os.environ.get("RR_BENCH_PRIO", "0")),
+                    help="1: run the extraction on a high-priority stream (the overlapped search keeps the default)")
     ap.add_argument("--tune", default="", help="developer A/B: rr_set_tuning pairs key=value[,key=value]")
     return ap.parse_args()
 
@@ -503,6 +505,10 @@ def main():
 
     ev_pairs = []
 
+    if args.extract_priority:
+        # extraction on a high-priority stream: the overlapped search (default
+        # priority) fills the extractor's gaps instead of competing with it
+        torch.cuda.set_stream(torch.cuda.Stream(dev, priority=-1))
     main_stream = torch.cuda.current_stream(dev)
     match_stream = torch.cuda.Stream(dev) if args.overlap else main_stream
 
