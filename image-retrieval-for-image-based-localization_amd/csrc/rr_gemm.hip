@@ -629,42 +629,56 @@ __global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int n
     const int grp = wave >> 2;              // wave group; also the 64-row half of each quadrant
     const int wn = wave & 3;                // 32-column quarter of each quadrant
     // XCD-contiguous bijective tile order (blocks are dispatched round-robin over 8 XCDs)
-    const int nwg = (int)gridDim.x, bx = (int)blockIdx.x;
-    const int xcd = bx & 7, q8 = nwg >> 3, r8 = nwg & 7;
-    const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bx >> 3);
-    if (t >= ntiles) return;
-    const int c0 = (t / tiles_p) * 256, p0 = (t % tiles_p) * 256;
+    // Persistent blocks over an XCD-contiguous tile order: XCD x (blocks are
+    // dispatched round-robin over the 8 XCDs) owns the contiguous tile range
+    // [s_x, s_x + n_x) and its nb_x blocks stride through it, so the tiles in
+    // flight on one XCD share A / B rows in its L2.  With one block per tile
+    // (grid = ntiles) this is the plain bijective remap.
+    const int nwg = (int)gridDim.x, bx = (int)blockIdx.x, xcd = bx & 7;
+    const int nt8 = ntiles >> 3, rt8 = ntiles & 7;
+    const int s_x = xcd < rt8 ? xcd * (nt8 + 1) : rt8 * (nt8 + 1) + (xcd - rt8) * nt8;
+    const int n_x = nt8 + (xcd < rt8 ? 1 : 0);
+    const int nb_x = (nwg >> 3) + (xcd < (nwg & 7) ? 1 : 0);
+    int li = bx >> 3;  // this block's local tile index on its XCD
+    if (li >= n_x) return;
     const int H = a.h, W = a.w_, Cin = a.cin;
     const int nk = a.kp / 64;
     const unsigned lds0 = (unsigned)(unsigned long long)smem;
     const int lrow = lane >> 3, lchunk = (lane & 7) ^ (lrow & 7);
 
-    // ---- LDS-DMA descriptors: half-tile h, instruction i covers rows (wave + 8 i) * 8 + lrow
-    const long long arows = min(256, a.cout - c0);
-    const i32x4_t rsA = make_rsrc((const char*)a.w + (long long)c0 * a.kp * ESZ, (unsigned)(arows * a.kp * ESZ));
+    // ---- per-tile LDS-DMA descriptors: half-tile h, instruction i covers rows (wave + 8 i) * 8 + lrow
     const i32x4_t rsB = make_rsrc(a.x, (unsigned)((long long)a.n * H * W * Cin * ESZ));
+    int c0 = 0, p0 = 0;
+    i32x4_t rsA;
     unsigned a_off[2][2], b_base[2][2];
     int b_hi[2][2], b_wi[2][2];
+    auto setup = [&](int t) {
+        c0 = (t / tiles_p) * 256;
+        p0 = (t % tiles_p) * 256;
+        const long long arows = min(256, a.cout - c0);
+        rsA = make_rsrc((const char*)a.w + (long long)c0 * a.kp * ESZ, (unsigned)(arows * a.kp * ESZ));
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+        for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int row = h * 128 + (wave + 8 * i) * 8 + lrow;
-            a_off[h][i] = row < arows ? (unsigned)(((long long)row * a.kp + lchunk * VEC) * ESZ) : OOB;
-            const int p = p0 + row;
-            if (p < a.P) {
-                const int img = p / (a.ho * a.wo);
-                const int rem = p - img * (a.ho * a.wo);
-                const int oh = rem / a.wo, ow = rem - oh * a.wo;
-                b_hi[h][i] = oh * a.stride - a.pad;
-                b_wi[h][i] = ow * a.stride - a.pad;
-                b_base[h][i] = (unsigned)((long long)img * H * W * Cin + ((long long)b_hi[h][i] * W + b_wi[h][i]) * Cin +
-                                          lchunk * VEC);
-            } else {
-                b_hi[h][i] = b_wi[h][i] = -(1 << 28);
-                b_base[h][i] = OOB;
+            for (int i = 0; i < 2; ++i) {
+                const int row = h * 128 + (wave + 8 * i) * 8 + lrow;
+                a_off[h][i] = row < arows ? (unsigned)(((long long)row * a.kp + lchunk * VEC) * ESZ) : OOB;
+                const int p = p0 + row;
+                if (p < a.P) {
+                    const int img = p / (a.ho * a.wo);
+                    const int rem = p - img * (a.ho * a.wo);
+                    const int oh = rem / a.wo, ow = rem - oh * a.wo;
+                    b_hi[h][i] = oh * a.stride - a.pad;
+                    b_wi[h][i] = ow * a.stride - a.pad;
+                    b_base[h][i] = (unsigned)((long long)img * H * W * Cin +
+                                              ((long long)b_hi[h][i] * W + b_wi[h][i]) * Cin + lchunk * VEC);
+                } else {
+                    b_hi[h][i] = b_wi[h][i] = -(1 << 28);
+                    b_base[h][i] = OOB;
+                }
             }
-        }
+    };
+    setup(s_x + li);
     // half-tile X (0 A0, 1 A1, 2 B0, 3 B1) of K-step kt into buffer buf; K-steps >= nk load zeros
     auto issue = [&](int X, int kt, int buf) {
         const unsigned dst = lds0 + (buf * 4 + X) * HT;
@@ -754,17 +768,24 @@ __global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int n
     auto bar = []() { asm volatile("s_barrier" ::: "memory"); };
 
     // ---- prologue: K-step 0 into E (A0 B1 A1 B0), K-step 1's A0 / B1 into O
-    issue(0, 0, 0);
-    issue(3, 0, 0);
-    issue(1, 0, 0);
-    issue(2, 0, 0);
-    issue(0, 1, 1);
-    issue(3, 1, 1);
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    bar();
-    if (grp == 1) bar();  // stagger: group 1 runs one barrier behind group 0
-
+    auto prologue = [&]() {
+        issue(0, 0, 0);
+        issue(3, 0, 0);
+        issue(1, 0, 0);
+        issue(2, 0, 0);
+        issue(0, 1, 1);
+        issue(3, 1, 1);
+    };
+    prologue();
     const int nit = (nk + 1) >> 1;
+    for (;;) {
+        // K-step 0 has landed: only the 4 youngest VMEM ops may still be in flight
+        // (K-step 1's A0 / B1, or the previous tile's last epilogue stores, which
+        // were issued after this tile's prologue)
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        bar();
+        if (grp == 1) bar();  // stagger: group 1 runs one barrier behind group 0
+
     for (int it = 0; it < nit; ++it) {
         const int te = 2 * it, to = 2 * it + 1;
         // phases 1-4: K-step te from E; loads: A1-O(to), B0-O(to), A0-E(te+2), B1-E(te+2)
@@ -788,9 +809,17 @@ __global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int n
         asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // K-step te + 2 (buffer E) has landed
         bar(); mfma_q(1, 0); bar();
     }
-    if (grp == 0) bar();  // equal barrier counts for both groups
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the block
+    if (grp == 0) bar();  // equal barrier counts for both groups: every wave's LDS reads are done
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing (zero) K-step DMAs have landed
 
+    // the next tile's prologue DMA flies while this tile's epilogue runs
+    const int ec0 = c0, ep0 = p0;
+    li += nb_x;
+    const bool more = li < n_x;
+    if (more) {
+        setup(s_x + li);
+        prologue();
+    }
     // ---- epilogue: folded BN scale / shift, residual, activation, NHWC store
     TO* __restrict__ Y = (TO*)a.y;
     const TO* __restrict__ R = (const TO*)a.res;
@@ -802,7 +831,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int n
         if constexpr (PERM) {
 #pragma unroll
             for (int i2 = 0; i2 < 2; ++i2) {
-                const int c = c0 + qa * 128 + grp * 64 + 32 * i2 + 8 * kq;  // 8 consecutive channels
+                const int c = ec0 + qa * 128 + grp * 64 + 32 * i2 + 8 * kq;  // 8 consecutive channels
                 if (c >= a.cout) continue;
                 float sc[8], sh[8];
                 if (affine) {
@@ -818,7 +847,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int n
                 for (int qb = 0; qb < 2; ++qb)
 #pragma unroll
                     for (int j = 0; j < 2; ++j) {
-                        const int p = p0 + qb * 128 + wn * 32 + j * 16 + r16;
+                        const int p = ep0 + qb * 128 + wn * 32 + j * 16 + r16;
                         if (p >= a.P) continue;
                         float v[8];
 #pragma unroll
@@ -854,7 +883,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int n
         } else {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const int c = c0 + qa * 128 + grp * 64 + i * 16 + 4 * kq;
+                const int c = ec0 + qa * 128 + grp * 64 + i * 16 + 4 * kq;
                 if (c >= a.cout) continue;
                 float sc[4] = {1.f, 1.f, 1.f, 1.f}, sh[4] = {0.f, 0.f, 0.f, 0.f};
                 const bool full = c + 3 < a.cout;
@@ -866,7 +895,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int n
                 for (int qb = 0; qb < 2; ++qb)
 #pragma unroll
                     for (int j = 0; j < 2; ++j) {
-                        const int p = p0 + qb * 128 + wn * 32 + j * 16 + r16;
+                        const int p = ep0 + qb * 128 + wn * 32 + j * 16 + r16;
                         if (p >= a.P) continue;
                         float v[4];
 #pragma unroll
@@ -903,9 +932,20 @@ __global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int n
             }
         }
     }
+#pragma unroll
+    for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[qa][qb][i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    if (!more) break;
+    }  // persistent tile loop
 }
 
 static int g_gemm8 = -1;  // rr_set_tuning(RR_TUNE_GEMM8) / RR_GEMM8: 0 off, 1 auto (default), 2 force where legal
+static bool g_gemm8_tile = false;  // RR_TUNE_GEMM8 value | 4: one block per tile instead of persistent blocks
 
 // 16-bit operands, 1x1 or tap-uniform im2col, an even number of 64-deep
 // K-steps, 31-bit operand offsets, and (auto) enough 256 x 256 tiles to fill
@@ -938,7 +978,16 @@ static bool try_gemm8(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
         const int km = k1 ? 1 : 2;
         const int tiles_p = (a.P + 255) / 256, tiles_c = (a.cout + 255) / 256;
         const long long ntiles = (long long)tiles_p * tiles_c;
-        const dim3 g((unsigned)ntiles), b(512);
+        // persistent blocks (one per CU walks its XCD's tile range, the next tile's
+        // prologue DMA overlapping this tile's epilogue) for the kNN score GEMM
+        // (Q = 1024: 5.386 / 5.390 -> 5.356 / 5.339 ms, same-box A/B); one block per
+        // tile for the convs, where persistence measured -0.3 % on the body
+        // (25.69 / 25.73 vs 25.77 / 26.13 ms).  RR_TUNE_GEMM8 = 2 forces persistence
+        // everywhere, | 4 forces one block per tile.
+        const long long cus = grid_cus();
+        const bool persist = !g_gemm8_tile && (g_gemm8 == 2 || !std::is_same<T, TO>::value);
+        // (a grid below 8 blocks would leave some XCD's tile range without a block)
+        const dim3 g((unsigned)(!persist || cus < 8 || ntiles < cus ? ntiles : cus)), b(512);
 #define RR_G8(KMV, PV) hipLaunchKernelGGL((k_gemm8<T, TO, KMV, PV>), g, b, 0, s, a, tiles_p, (int)ntiles)
         if constexpr (std::is_same<T, TO>::value) {
             if (perm) {
@@ -1012,7 +1061,11 @@ void set_gemm_tuning(int key, int value) {
     else if (key == RR_TUNE_GEMM_WIDE) g_wide = value != 0;
     else if (key == RR_TUNE_GEMM_ASTAT) g_ast = value != 0;
     else if (key == RR_TUNE_GEMM_XCD_MAP) g_xmap = value != 0;
-    else if (key == RR_TUNE_GEMM8) g_gemm8 = value < 0 ? 0 : value > 2 ? 2 : value;
+    else if (key == RR_TUNE_GEMM8) {
+        g_gemm8_tile = value >= 0 && (value & 4);
+        value = value < 0 ? 0 : value & 3;
+        g_gemm8 = value > 2 ? 2 : value;
+    }
 }
 
 template void launch_gemm2<bf16_t, bf16_t>(const ConvArgs&, bool, hipStream_t);

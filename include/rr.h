@@ -276,7 +276,9 @@ int rr_mutual_nn(const long long* nn12, int n1, const long long* nn21, int n2, l
  *   RR_TUNE_GRID_CUS     cap on the CUs one persistent launch spreads over
  *                        (0 = all; e.g. half the chip for two concurrent streams)
  *   RR_TUNE_GEMM8        0 off, 1 auto, 2 forced: the 8-phase staggered 256x256 GEMM for eligible
- *                        16-bit 1x1 / tap-uniform convs and score GEMMs (default 1)
+ *                        16-bit 1x1 / tap-uniform convs and score GEMMs (default 1: persistent
+ *                        blocks for the kNN score GEMM, one block per tile for convs; 2: also
+ *                        persistent everywhere; | 4: one block per tile everywhere)
  *   RR_TUNE_KNN_FUSED    0/1 kNN screening in the score-GEMM epilogue after a 4-chunk
  *                        prefix (default 1); 0 = every chunk through the score slab
  *   RR_TUNE_CONV3_PIPE   1 (default): the direct 3x3 kernel reads the operands of its next

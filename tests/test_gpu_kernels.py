@@ -602,3 +602,38 @@ def test_gemm8_bit_identical_to_tiled_engine(cuda, shape, prec):
         E.lib().rr_set_tuning(6, 1)
         E.lib().rr_set_tuning(5, 1)
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("cap", [0, 9, 37])
+@pytest.mark.parametrize("shape", [(16, 48, 64, 1024, 256, 1, 1), (16, 24, 32, 512, 2048, 1, 1),
+                                   (16, 48, 64, 256, 256, 3, 1)])
+def test_gemm8_persistent_equals_one_block_per_tile(cuda, shape, cap):
+    """Persistent k_gemm8 blocks (each walks its XCD's tile range, the next tile's
+    prologue DMA overlapping the epilogue) vs one block per tile (RR_TUNE_GEMM8 | 4):
+    bit-identical, also with grid caps that give the XCDs unequal block counts and
+    a residual epilogue."""
+    from cirtorch import _engine as E
+    n, h, w, cin, cout, k, s = shape
+    g = torch.Generator(device=cuda).manual_seed(11)
+    x = torch.randn((n, h, w, cin), generator=g, device=cuda).to(torch.bfloat16)
+    wt = torch.randn((cout, cin, k, k), generator=g, device=cuda) * (2.0 / (cin * k * k)) ** 0.5
+    wp = _ops().pack_conv_weights(wt, cin, torch.bfloat16, perm32=True)
+    sc = torch.rand(cout, generator=g, device=cuda) + 0.5
+    sh = torch.randn(cout, generator=g, device=cuda) * 0.1
+    p = 1 if k == 3 else 0
+    res = torch.randn((n, h, w, cout), generator=g, device=cuda).to(torch.bfloat16) if k == 1 else None
+    E.check(E.lib().rr_set_tuning(6, 0), "rr_set_tuning")
+    E.check(E.lib().rr_set_tuning(5, 0), "rr_set_tuning")
+    try:
+        E.check(E.lib().rr_set_tuning(8, 2 | 4), "rr_set_tuning")
+        ref = _ops().conv2d_fused(x, wp, k, k, s, p, cout, sc, sh, residual=res, leaky=True, perm32=True)
+        E.check(E.lib().rr_set_tuning(8, 2), "rr_set_tuning")
+        E.check(E.lib().rr_set_tuning(7, cap), "rr_set_tuning")
+        got = _ops().conv2d_fused(x, wp, k, k, s, p, cout, sc, sh, residual=res, leaky=True, perm32=True)
+    finally:
+        E.lib().rr_set_tuning(7, 0)
+        E.lib().rr_set_tuning(8, 1)
+        E.lib().rr_set_tuning(6, 1)
+        E.lib().rr_set_tuning(5, 1)
+    assert torch.equal(got, ref)
+
