@@ -472,6 +472,249 @@ __global__ void __launch_bounds__(NT) k_stem_pool2(StemArgs a, int tiles_w, int 
 }
 
 
+// ---------------------------------------------------------------------------
+// Stem v3: the v2 tile and pool-before-epilogue, with the MFMA operands
+// swapped so pooling and the epilogue run lane-locally on useful values only.
+// A = 16 stem pixels (rows), B = 16 output channels (columns): lane (j, q)
+// holds pixels 4q..4q+3 of output channel 4j + f in fragment f.  The wave's
+// 16 pixels are stem columns 14w + 4q + e: group q pools pooled columns
+// 7w + 2q (its pixels e = 0,1,2) and 7w + 2q + 1 (e = 2,3 and pixel e = 0 of
+// group q + 1, one ds_bpermute from lane + 16; group 3's second column belongs
+// to the next wave and is dropped).  Per pooled row a lane runs 16 + 8 max3,
+// BN + activation on 8 values (4 consecutive channels of 2 pooled pixels) and
+// two 8-B stores -- v2 shifted 32 values by DPP and ran the epilogue on every
+// lane of which 7 of 16 stored.  Per-lane channel constants live in VGPRs.
+// Patch fill: float pixels are normalised as packed pairs (v_pk_add/mul_f32,
+// the same IEEE operations); uint8 pixels go through a per-channel LDS table
+// of the normalised value of each byte (x / 255 in IEEE division, then the
+// same normalisation), computed once per block.  Same values as v2 bit for
+// bit when the swapped MFMA accumulates in the same order.
+template <typename HT, bool U8, int NPART>
+__global__ void __launch_bounds__(NT) k_stem_pool3(StemArgs a, int tiles_w, int tiles_hw, int ntiles) {
+    constexpr int PH = 8, PW = 56, SRN = 2 * PH + 1, CB = 14;
+    constexpr int IR = 2 * (SRN - 1) + 7;            // 39 input rows
+    constexpr int SCN = CB * 7 + 16;                 // 114 stem columns
+    constexpr int IC = 2 * (SCN - 1) + 8;            // 234 input columns (even: 16-B pixel pairs)
+    constexpr int HIC = IC / 2;
+    constexpr int NPAIR = IR * HIC, PPT = (NPAIR + NT - 1) / NT;
+    constexpr int PATCH = IR * IC * 8;
+    static_assert(PW == 7 * (NT / 64), "one 7-pooled-column block per wave");
+    typedef __attribute__((ext_vector_type(2))) float f2;
+    __shared__ __attribute__((aligned(16))) char sP[2][PATCH];
+    __shared__ float sL[U8 ? 3 * 256 : 1];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r16 = lane & 15, q = lane >> 4;
+    const int H = a.h, W = a.w_;
+    const long long plane = (long long)H * W;
+
+    if constexpr (U8) {
+        for (int i = tid; i < 3 * 256; i += NT) {
+            const int ch = i >> 8;
+            const float x = (float)(i & 255) / 255.f;  // IEEE division = to_tensor
+            sL[i] = a.do_norm ? (x - a.mean[ch]) * a.rstd[ch] : x;
+        }
+    }
+    // B fragments: channel 4 * r16 + f of fragment f, K-step m = kernel row m;
+    // negative-scale channels negated (pool before the epilogue, see v2)
+    uint4 breg[4][7];
+    float sc[4], sh[4];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+        const int c = 4 * r16 + f;
+        const int R = (c & ~31) | (((c >> 2) & 1) << 4) | (((c >> 3) & 3) << 2) | (c & 3);  // perm32_channel^-1
+        const float s = a.scale[c];
+        sc[f] = fabsf(s);
+        sh[f] = a.shift[c];
+        const unsigned flip = s < 0.f ? 0x80008000u : 0u;
+#pragma unroll
+        for (int m = 0; m < 7; ++m) {
+            uint4 w = a.w[R * 32 + m * 4 + q];
+            w.x ^= flip; w.y ^= flip; w.z ^= flip; w.w ^= flip;
+            breg[f][m] = w;
+        }
+    }
+
+    auto tile_origin = [&](int t, int& img, int& ph0, int& pw0) {
+        img = t / tiles_hw;
+        const int rem = t - img * tiles_hw;
+        const int th = rem / tiles_w;
+        ph0 = th * PH;
+        pw0 = (rem - th * tiles_w) * PW;
+    };
+
+    // patch fill in NPART parts, so only a third of the raw pixels is live in
+    // VGPRs while the MFMAs run (v2's halves spilled ~30 VGPRs)
+    constexpr int PH1 = (PPT + NPART - 1) / NPART;
+    typedef typename std::conditional<U8, int, float>::type PT;
+    PT pf[PH1][6];
+    auto fill_load = [&](int t, int half) {
+        int img, ph0, pw0;
+        tile_origin(t, img, ph0, pw0);
+        const int ir0 = 4 * ph0 - 5, ic0 = 4 * pw0 - 5;
+        constexpr int ESZ = U8 ? 1 : 4;
+        constexpr unsigned OOBO = 0x80000000u;
+        const char* ib = (const char*)a.x + (long long)img * 3 * plane * ESZ;
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc((void*)ib, (short)0, (int)(3 * plane * ESZ), 0x00020000);
+#pragma unroll
+        for (int uu = 0; uu < PH1; ++uu) {
+            const int u = half * PH1 + uu;
+            if (u >= PPT) break;
+            int k = tid + NT * u;
+            asm volatile("" : "+v"(k));  // offsets computed here, not hoisted into live VGPRs
+            const int kk = k < NPAIR ? k : NPAIR - 1;
+            const int r = kk / HIC, c = 2 * (kk - r * HIC);
+            const int ih = ir0 + r, iw = ic0 + c;
+            const bool rok = (unsigned)ih < (unsigned)H;
+            const int o = (ih * W + iw) * ESZ;
+            const unsigned off0 = rok && (unsigned)iw < (unsigned)W ? (unsigned)o : OOBO;
+            const unsigned off1 = rok && (unsigned)(iw + 1) < (unsigned)W ? (unsigned)(o + ESZ) : OOBO;
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) {
+                const unsigned po = (unsigned)(ch * (int)plane * ESZ);
+                if constexpr (U8) {
+                    pf[uu][2 * ch] = ch * 256 + (int)__builtin_amdgcn_raw_buffer_load_b8(rs, (int)(off0 + po), 0, 0);
+                    pf[uu][2 * ch + 1] = ch * 256 + (int)__builtin_amdgcn_raw_buffer_load_b8(rs, (int)(off1 + po), 0, 0);
+                } else {
+                    pf[uu][2 * ch] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(off0 + po), 0, 0));
+                    pf[uu][2 * ch + 1] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(off1 + po), 0, 0));
+                }
+            }
+        }
+    };
+    auto fill_store = [&](int t, int buf, int half) {
+        int img, ph0, pw0;
+        tile_origin(t, img, ph0, pw0);
+        const int ir0 = 4 * ph0 - 5, ic0 = 4 * pw0 - 5;
+#pragma unroll
+        for (int uu = 0; uu < PH1; ++uu) {
+            const int u = half * PH1 + uu;
+            if (u >= PPT) break;
+            int k = tid + NT * u;
+            asm volatile("" : "+v"(k));
+            if (k >= NPAIR) continue;
+            const int r = k / HIC, c = 2 * (k - r * HIC);
+            const bool rok = (unsigned)(ir0 + r) < (unsigned)H;
+            const bool ok0 = rok && (unsigned)(ic0 + c) < (unsigned)W;
+            const bool ok1 = rok && (unsigned)(ic0 + c + 1) < (unsigned)W;
+            f2 v[3];
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) {  // zero padding is applied AFTER normalisation
+                f2 x;
+                if constexpr (U8) {
+                    x = (f2){sL[pf[uu][2 * ch]], sL[pf[uu][2 * ch + 1]]};
+                } else {
+                    x = (f2){pf[uu][2 * ch], pf[uu][2 * ch + 1]};
+                    if (a.do_norm) x = (x - (f2){a.mean[ch], a.mean[ch]}) * (f2){a.rstd[ch], a.rstd[ch]};
+                }
+                v[ch] = (f2){ok0 ? x.x : 0.f, ok1 ? x.y : 0.f};
+            }
+            uint4 o;
+            o.x = H16<HT>::pack2(v[0].x, v[1].x);
+            o.y = H16<HT>::pack2(v[2].x, 0.f);
+            o.z = H16<HT>::pack2(v[0].y, v[1].y);
+            o.w = H16<HT>::pack2(v[2].y, 0.f);
+            *reinterpret_cast<uint4*>(sP[buf] + (r * IC + c) * 8) = o;
+        }
+    };
+
+    const float slope = a.leaky ? a.slope : 1.f;  // identity == leaky with slope 1
+    const float NINF = -__builtin_inff();
+    int t = blockIdx.x;
+    if (t >= ntiles) return;
+    if constexpr (U8) __syncthreads();  // byte table
+#pragma unroll
+    for (int part = 0; part < NPART; ++part) {
+        fill_load(t, part);
+        fill_store(t, 0, part);
+    }
+    __syncthreads();
+    const int nb_addr = ((lane + 16) & 63) * 4;
+    int cur = 0;
+    for (; t < ntiles; t += gridDim.x, cur ^= 1) {
+        const int tn = t + gridDim.x;
+        if (tn < ntiles) fill_load(tn, 0);
+        int img, ph0, pw0;
+        tile_origin(t, img, ph0, pw0);
+        const char* pb = sP[cur] + (2 * (CB * wave + r16) + 2 * q) * 8;
+        const bool active = pw0 + 7 * wave < a.wp;
+        // even stem dims (host-checked): the only stem pixels outside the map that
+        // feed stored outputs are row -1 (top tiles) and column -1 (left tiles:
+        // wave 0, pixel 0 = lanes of group 0, element 0)
+        const bool left = pw0 == 0 && wave == 0;
+        const int pc0 = 7 * wave + 2 * q;
+        const bool st0 = pw0 + pc0 < a.wp, st1 = q < 3 && pw0 + pc0 + 1 < a.wp;
+        auto stem_row = [&](int r, h16_f32x4_t (&acc)[4]) {
+#pragma unroll
+            for (int f = 0; f < 4; ++f) acc[f] = (h16_f32x4_t){0.f, 0.f, 0.f, 0.f};
+            const char* rb = pb + r * (2 * IC * 8);
+#pragma unroll
+            for (int m = 0; m < 7; ++m) {
+                const uint4 px = *reinterpret_cast<const uint4*>(rb + m * IC * 8);
+#pragma unroll
+                for (int f = 0; f < 4; ++f) acc[f] = H16<HT>::mfma(px, breg[f][m], acc[f]);
+            }
+        };
+        h16_f32x4_t A[4];
+        if (active) {
+            stem_row(0, A);
+            if (ph0 == 0) {  // stem row -1: max-pool padding
+#pragma unroll
+                for (int f = 0; f < 4; ++f) A[f] = (h16_f32x4_t){NINF, NINF, NINF, NINF};
+            }
+        }
+        for (int pr = 0; pr < PH; ++pr) {
+#pragma unroll
+            for (int part = 1; part < NPART; ++part)
+                if (pr == part * PH / NPART && tn < ntiles) {  // part - 1 of the next patch -> LDS, part in flight
+                    fill_store(tn, cur ^ 1, part - 1);
+                    fill_load(tn, part);
+                }
+            if (active) {
+                h16_f32x4_t B[4];
+                stem_row(2 * pr + 1, B);
+#pragma unroll
+                for (int f = 0; f < 4; ++f)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) A[f][e] = fmaxf(A[f][e], B[f][e]);  // rows 2pr, 2pr+1
+                h16_f32x4_t C[4];
+                stem_row(2 * pr + 2, C);
+                float p0[4], p1[4];
+#pragma unroll
+                for (int f = 0; f < 4; ++f) {
+                    float m3[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) m3[e] = fmaxf(A[f][e], C[f][e]);
+                    if (left && q == 0) m3[0] = NINF;  // stem column -1: max-pool padding
+                    const float nb = __int_as_float(__builtin_amdgcn_ds_bpermute(nb_addr, __float_as_int(m3[0])));
+                    p0[f] = fmaxf(fmaxf(m3[0], m3[1]), m3[2]);
+                    p1[f] = fmaxf(fmaxf(m3[2], m3[3]), nb);
+                    A[f] = C[f];
+                }
+                if (ph0 + pr < a.hp) {
+                    bf16_t* dst = a.y + (((long long)img * a.hp + ph0 + pr) * a.wp + pw0 + pc0) * 64 + 4 * r16;
+                    auto epi = [&](const float (&p)[4]) {
+                        float v[4];
+#pragma unroll
+                        for (int f = 0; f < 4; ++f) {
+                            v[f] = p[f] * sc[f] + sh[f];
+                            v[f] = fmaxf(v[f], v[f] * slope);
+                        }
+                        return make_uint2(H16<HT>::pack2(v[0], v[1]), H16<HT>::pack2(v[2], v[3]));
+                    };
+                    if (st0) *reinterpret_cast<uint2*>(dst) = epi(p0);
+                    if (st1) *reinterpret_cast<uint2*>(dst + 64) = epi(p1);
+                }
+            }
+        }
+        if (tn < ntiles) fill_store(tn, cur ^ 1, NPART - 1);
+        __syncthreads();
+    }
+}
+
+
 // out[R][k], R packed row (PERM32), k = kh*32 + kw*4 + ci (kh < 7, kw < 7, ci < 3 real; rest 0)
 template <typename HT>
 __global__ void k_stem_pack(const float* __restrict__ w, HT* __restrict__ out) {
@@ -506,7 +749,8 @@ extern "C" int rr_stem_pack_weights(const float* w, int c_out, int c_in, int kh,
 }
 
 namespace rr {
-int g_stem_mode = 1;  // rr_set_tuning(RR_TUNE_STEM): 1 pool-before-epilogue kernel (v2), 0 k_stem_pool
+int g_stem_mode = 2;  // rr_set_tuning(RR_TUNE_STEM): 2 swapped-operand lane-local pooling (v3),
+                      // 1 pool-before-epilogue kernel (v2), 0 k_stem_pool
 }
 
 template <bool U8>
@@ -538,12 +782,28 @@ static int stem_conv_pool(const void* x, int n, int h, int w, const float* mean_
     if (a.leaky && !(slope >= 0.f && slope <= 1.f)) return fail(RR_EINVAL, "rr_stem_conv_pool: leaky slope must be in [0, 1]");
     a.slope = slope;
     const int g_stem_cus = grid_cus();
-    if (g_stem_mode == 1 && ho % 2 == 0 && wo % 2 == 0) {  // v2 handles the even stem maps (borders top / left)
+    if (g_stem_mode >= 1 && ho % 2 == 0 && wo % 2 == 0) {  // v2/v3 handle the even stem maps (borders top / left)
         constexpr int PH = 8, PW = 56;
         const int tiles_w = (wp + PW - 1) / PW, tiles_h = (hp + PH - 1) / PH;
         const long long ntiles = (long long)n * tiles_h * tiles_w;
         if (ntiles >= (1ll << 31)) return fail(RR_EINVAL, "rr_stem_conv_pool: too many tiles");
         const int grid = (int)(ntiles < g_stem_cus ? ntiles : g_stem_cus);
+        if (g_stem_mode >= 2) {  // 2: patch fill in 3 parts (default), 3: 2 parts, 4: 5 parts
+            auto launch = [&](auto kern) {
+                hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), 0, as_stream(stream), a, tiles_w, tiles_w * tiles_h,
+                                   (int)ntiles);
+            };
+            if (dtype == RR_F16) {
+                if (g_stem_mode == 3) launch(k_stem_pool3<f16_t, U8, 2>);
+                else if (g_stem_mode == 4) launch(k_stem_pool3<f16_t, U8, 5>);
+                else launch(k_stem_pool3<f16_t, U8, 3>);
+            } else {
+                if (g_stem_mode == 3) launch(k_stem_pool3<bf16_t, U8, 2>);
+                else if (g_stem_mode == 4) launch(k_stem_pool3<bf16_t, U8, 5>);
+                else launch(k_stem_pool3<bf16_t, U8, 3>);
+            }
+            return check_launch("rr_stem_conv_pool");
+        }
         if (dtype == RR_F16)
             hipLaunchKernelGGL((k_stem_pool2<f16_t, U8>), dim3(grid), dim3(NT), 0, as_stream(stream), a, tiles_w,
                                tiles_w * tiles_h, (int)ntiles);

@@ -336,7 +336,7 @@ def test_stem_conv_pool(cuda, dt, shape, norm):
 @pytest.mark.parametrize("shape", [(2, 61, 83), (1, 96, 470), (3, 200, 130)])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 def test_stem_pool_before_epilogue_bit_identical(cuda, dt, shape):
-    """RR_TUNE_STEM: the v2 stem pools the raw conv and applies BN + leaky +
+    """RR_TUNE_STEM: the v2 / v3 stems pool the raw conv and applies BN + leaky +
     rounding to the pooled pixels only (exact: the epilogue is non-decreasing
     once negative-scale rows are negated).  Positive- and zero-scale channels
     are bit-identical to the v1 kernel; negative-scale channels differ only
@@ -358,12 +358,12 @@ def test_stem_pool_before_epilogue_bit_identical(cuda, dt, shape):
     xu = (x * 255).to(torch.uint8)
     outs = {}
     try:
-        for mode in (0, 1):
+        for mode in (0, 1, 2):
             E.check(E.lib().rr_set_tuning(11, mode), "rr_set_tuning")
             outs[mode] = [ops.stem_conv_pool(inp.to(cuda), wpk, scale.to(cuda), shift.to(cuda), leaky=True,
                                              slope=0.01, mean=mean, std=std).float().cpu() for inp in (x, xu)]
     finally:
-        E.lib().rr_set_tuning(11, 1)
+        E.lib().rr_set_tuning(11, 2)
     neg = scale < 0
     ulp = 2.0 ** -7 if dt == torch.bfloat16 else 2.0 ** -10
     for a, b in zip(outs[0], outs[1]):
@@ -371,6 +371,9 @@ def test_stem_pool_before_epilogue_bit_identical(cuda, dt, shape):
         d = (a[..., neg] - b[..., neg]).abs()
         assert (d > 0).float().mean().item() < 1e-3
         assert (d <= ulp * a[..., neg].abs().clamp_min(1.0)).all()
+    # v3 (swapped MFMA operands, lane-local pooling, byte table for uint8) == v2
+    for b, c in zip(outs[1], outs[2]):
+        assert torch.equal(b, c), (b - c).abs().max().item()
 
 
 @pytest.mark.parametrize("c_out", [64, 128])

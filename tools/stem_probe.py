@@ -13,6 +13,7 @@ def main():
     import argparse
     ap = argparse.ArgumentParser()
     ap.add_argument("--tune", default="", help="rr_set_tuning pairs key=value[,key=value]")
+    ap.add_argument("--u8", action="store_true", help="uint8 pixels (rr_stem_conv_pool_u8)")
     args = ap.parse_args()
     from cirtorch import _ops
     from cirtorch import _engine as E
@@ -20,6 +21,8 @@ def main():
         k_, v_ = kv.split("=")
         E.check(E.lib().rr_set_tuning(int(k_), int(v_)), "rr_set_tuning")
     x = torch.rand(32, 3, 768, 1024, device="cuda")
+    if args.u8:
+        x = (x * 255).to(torch.uint8)
     w = torch.randn(64, 3, 7, 7, device="cuda") * 0.1
     wp = _ops.pack_stem_weights(w)
     sc, sh = torch.rand(64, device="cuda") + 0.5, torch.randn(64, device="cuda") * 0.1
@@ -33,7 +36,7 @@ def main():
         _ops.stem_conv_pool(x, wp, sc, sh, mean=mean, std=std)
     b.record()
     torch.cuda.synchronize()
-    print("stem: %.1f us/launch" % (a.elapsed_time(b) * 100))
+    print("stem %s %s: %.1f us/launch (32 images)" % (args.tune, "u8" if args.u8 else "f32", a.elapsed_time(b) * 100))
 
 
 if __name__ == "__main__":
