@@ -675,7 +675,7 @@ void launch_s_t(const ConvArgs& a, hipStream_t s) {
 
 }  // namespace
 
-int g_stream_mode = 1;  // rr_set_tuning(RR_TUNE_STREAM_1X1): 0 off, 1 auto
+int g_stream_mode = 1;  // rr_set_tuning(RR_TUNE_STREAM_1X1): 0 off, 1 auto, 2 / 3 see launch_stream1x1
 
 // bf16 1x1 (pad 0, any stride), PERM32 weights, bf16 out: returns false when the
 // shape is not one the streaming kernel is built for (caller uses the tiled engine).
@@ -693,6 +693,10 @@ bool launch_stream1x1(const ConvArgs& a, hipStream_t s, bool f16) {
     if (a.P < 4096 || (long long)a.n * a.h * a.w_ * a.cin >= (1ll << 31)) return false;
     const bool res = a.flags & RR_CONV_RESIDUAL;
     const int K = a.cin, C = a.cout;
+    // mode 2: the residual 512 -> 2048 1x1 (mod5 conv3) on the 8-phase GEMM;
+    // mode 3: also the residual 256 -> 1024 1x1 (mod4 conv3)
+    if (g_stream_mode >= 2 && K == 512 && C == 2048 && res && gemm8_eligible(a, true, 2)) return false;
+    if (g_stream_mode >= 3 && K == 256 && C == 1024 && res && gemm8_eligible(a, true, 2)) return false;
     if (K == 64 && C == 64) { launch_s<64, 64, 2, 4, 8>(a, s, f16); return true; }
     if (K == 64 && C == 256) { launch_s<256, 64, 1, 2, 8>(a, s, f16); return true; }
     if (K == 256 && C == 64) { launch_s<64, 256, 1, 4, 8>(a, s, f16); return true; }

@@ -607,6 +607,38 @@ def test_gemm8_bit_identical_to_tiled_engine(cuda, shape, prec):
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("shape", [(128, 24, 32, 512, 2048), (64, 48, 64, 256, 1024), (3, 17, 29, 512, 512)])
+@pytest.mark.parametrize("leaky", [True, False])
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_gemm8_residual_epilogue_bit_identical(cuda, shape, leaky, prec):
+    """Residual 1x1s (mod5 / mod4 conv3 shapes, a ragged one) through k_gemm8's
+    branch-free buffer-op epilogue (scale / shift via LDS, residual prefetched,
+    act = max(v, slope v)) vs the tiled engine: bit-identical."""
+    from cirtorch import _engine as E
+    n, h, w, cin, cout = shape
+    g = torch.Generator(device=cuda).manual_seed(13)
+    dt = torch.bfloat16 if prec == "bf16" else torch.float16
+    x = torch.randn((n, h, w, cin), generator=g, device=cuda).to(dt)
+    wt = torch.randn((cout, cin, 1, 1), generator=g, device=cuda) * (2.0 / cin) ** 0.5
+    wp = _ops().pack_conv_weights(wt, cin, dt, perm32=True)
+    sc = torch.rand(cout, generator=g, device=cuda) + 0.5
+    sc[::7] *= -1.0
+    sh = torch.randn(cout, generator=g, device=cuda) * 0.1
+    res = torch.randn((n, h, w, cout), generator=g, device=cuda).to(dt)
+    E.check(E.lib().rr_set_tuning(6, 0), "rr_set_tuning")
+    E.check(E.lib().rr_set_tuning(5, 0), "rr_set_tuning")
+    try:
+        E.check(E.lib().rr_set_tuning(8, 2), "rr_set_tuning")
+        a = _ops().conv2d_fused(x, wp, 1, 1, 1, 0, cout, sc, sh, residual=res, leaky=leaky, perm32=True)
+        E.check(E.lib().rr_set_tuning(8, 0), "rr_set_tuning")
+        b = _ops().conv2d_fused(x, wp, 1, 1, 1, 0, cout, sc, sh, residual=res, leaky=leaky, perm32=True)
+    finally:
+        E.lib().rr_set_tuning(8, 1)
+        E.lib().rr_set_tuning(6, 1)
+        E.lib().rr_set_tuning(5, 1)
+    assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("cap", [0, 9, 37])
 @pytest.mark.parametrize("shape", [(16, 48, 64, 1024, 256, 1, 1), (16, 24, 32, 512, 2048, 1, 1),
                                    (16, 48, 64, 256, 256, 3, 1)])
