@@ -754,9 +754,11 @@ def main():
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                      "frac": achieved / peak, "traffic": traffic, "traffic_note": traffic_note,
                      "algorithmic_bytes": bytes_img * B,
-                     "note": "dominant kernel family = the extractor body's 53 conv launches per forward (k_stem_pool, "
-                             "k_conv3x3, k_stream1x1, k_igemm; their per-kernel rocprof averages sum to this time, "
-                             "see profiles/); "
+                     "note": "dominant kernel family = the extractor body's 53 conv layers per forward (k_stem_pool3, "
+                             "k_gemm8, k_conv3x3, k_stream1x1, fused boundaries k_stream_pair / k_pair_mid, k_igemm; "
+                             "their per-kernel rocprof averages sum to this time, see profiles/); algorithmic_bytes = "
+                             "per-layer unfused input + output (+ residual) bytes, so the fused boundaries can bring "
+                             "the PMC traffic below it; "
                              "%.2f GFLOP/img x %d img / extract-body event time %.3f ms" % (fl_img / 1e9, B, body_ms)},
         "roofline_layers": {"floor_ms": floor_ms, "measured_ms": body_ms, "frac": floor_ms / body_ms,
                             "hbm_bytes_per_img": bytes_img, "peak_mfma_tflops": peak_m / 1e12,
