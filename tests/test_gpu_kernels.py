@@ -333,7 +333,10 @@ def test_stem_conv_pool(cuda, dt, shape, norm):
     assert (got == un).float().mean().item() > 0.95
 
 
-@pytest.mark.parametrize("shape", [(2, 61, 83), (1, 96, 470), (3, 200, 130)])
+# odd stem maps take the v1 kernel in every mode; even ones (2, 64, 84), (1, 100, 472),
+# (3, 200, 132) the v2 / v3 tiles (partial wave strips, several tiles both ways)
+@pytest.mark.parametrize("shape", [(2, 61, 83), (1, 96, 470), (3, 200, 130), (2, 64, 84), (1, 100, 472),
+                                   (3, 200, 132)])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 def test_stem_pool_before_epilogue_bit_identical(cuda, dt, shape):
     """RR_TUNE_STEM: the v2 / v3 stems pool the raw conv and applies BN + leaky +
