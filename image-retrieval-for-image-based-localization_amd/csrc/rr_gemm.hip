@@ -1038,8 +1038,10 @@ void launch_gemm2(const ConvArgs& a, bool k1, hipStream_t s) {
         launch_cfg3<T, TO, 256, 32, 4, 1>(a, k1, perm, s);
     else if (a.P <= 64)
         launch_cfg3<T, TO, 256, 64, 4, 1>(a, k1, perm, s);
-    else if (a.P <= 128 && a.cout >= 4096)  // kNN score GEMM at 65..128 queries: no half-empty 256-wide pixel tiles
-        launch_cfg3<T, TO, 256, 128, 4, 2>(a, k1, perm, s);
+    else if (a.P <= 128 && a.cout >= 4096)  // kNN score GEMM at 65..128 queries: no half-empty 256-wide pixel tiles;
+        // 128 x 128 (4 waves, 64 KiB: two blocks per CU) measured 1.296 / 1.306 vs 1.328 / 1.335 ms for the
+        // Q = 128 search against 1M x 2048 with 256 x 128 (tools/knn_cfg_ab.sh)
+        launch_cfg3<T, TO, 128, 128, 2, 2>(a, k1, perm, s);
     else if (a.cout <= 64)
         launch_cfg3<T, TO, 64, 256, 1, 4>(a, k1, perm, s);
     else if (a.cout <= 128 || !g_wide)
