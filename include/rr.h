@@ -267,7 +267,8 @@ int rr_mutual_nn(const long long* nn12, int n1, const long long* nn21, int n2, l
  *   RR_TUNE_GEMM_ASTAT   0/1 allow the A-stationary tiles in the automatic choice
  *   RR_TUNE_GEMM_XCD_MAP 0/1 XCD-contiguous tile order (default 0)
  *   RR_TUNE_STREAM_1X1   0/1 weight-stationary streaming kernel for the
- *                        HBM-bound bf16 1x1 convs (default 1)
+ *                        HBM-bound bf16 1x1 convs (default 1); 2 / 3 also route the
+ *                        residual 512->2048 / 256->1024 1x1s to the 8-phase GEMM (A/B only)
  *   RR_TUNE_CONV3X3      0 off, 1 auto (default): direct 3x3 kernel with LDS
  *                        halo patches for the bf16 stride-1 3x3 convs;
  *                        2 / 3 prefer its 8x32 / 4x32 pixel tiles, 4 / 6 use
@@ -283,8 +284,10 @@ int rr_mutual_nn(const long long* nn12, int n1, const long long* nn21, int n2, l
  *                        prefix (default 1); 0 = every chunk through the score slab
  *   RR_TUNE_CONV3_PIPE   1 (default): the direct 3x3 kernel reads the operands of its next
  *                        half-step while the current one's MFMAs issue; 0: compiler schedule
- *   RR_TUNE_STEM         1 (default): fused stem pools the raw conv before BN/activation
- *                        (exact by monotonicity); 0: BN/activation on every stem pixel
+ *   RR_TUNE_STEM         2 (default): fused stem v3 (pixels x channels MFMA, lane-local
+ *                        pooling; 3 / 4: patch fill in 2 / 5 parts); 1: v2 (pools the raw
+ *                        conv before BN/activation, exact by monotonicity); 0: v1 (BN/activation
+ *                        on every stem pixel).  Odd stem maps always take v1.
  *   RR_TUNE_STREAM_XCD   1 (default): the streaming 1x1's channel-slice blocks of one pixel
  *                        strip run on one XCD (the strip's input is re-read from that L2) */
 enum rr_tune_key { RR_TUNE_GEMM_CONFIG = 0, RR_TUNE_GEMM_STAGES = 1, RR_TUNE_GEMM_WIDE = 2,
