@@ -944,6 +944,164 @@ __global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int n
     }  // persistent tile loop
 }
 
+// ---------------------------------------------------------------------------
+// Half-width 8-phase variant for the kNN score GEMM at <= 128 queries: a
+// 256 (database rows, A) x 128 (queries, B) tile, so no MFMA runs on empty
+// query rows (k_gemm8's 256-wide pixel tile would waste half of them).
+// Same wave layout, quadrant phases and one-barrier wave-group stagger as
+// k_gemm8, with two phases per 64-deep K-step (A0 x B0, A1 x B0; the B
+// fragments stay in registers for the second) and a 3-stage ring of
+// {A0, A1, B0} half-tiles (144 KiB): K-step t + 2's A0 / B0 are issued in
+// phase A of t and its A1 in phase B of t, into the stage K-step t - 1 used --
+// every half-tile is overwritten two phases after its last read (the k_gemm8
+// rule that keeps the skewed group's reads safe) and has four phases to land.
+// Counted waits (2 DMA instructions per half-tile and lane): phase A waits for
+// this K-step's A1 (10 younger), phase B for the next K-step's A0 / B0 (8).
+template <typename T>
+__global__ void __launch_bounds__(512, 1) k_gemm8h(ConvArgs a, int ntiles) {
+    static_assert(sizeof(T) == 2, "16-bit operands");
+    constexpr int VEC = 8, ESZ = 2, HT = 16384, ST = 3 * HT;  // stage = [A0, A1, B0]
+    __shared__ __attribute__((aligned(1024))) char smem[3 * ST];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wave >> 2, wn = wave & 3;
+    // XCD-contiguous bijective tile order (one block per tile)
+    const int bx = (int)blockIdx.x, xcd = bx & 7;
+    const int nt8 = ntiles >> 3, rt8 = ntiles & 7;
+    const int t = (xcd < rt8 ? xcd * (nt8 + 1) : rt8 * (nt8 + 1) + (xcd - rt8) * nt8) + (bx >> 3);
+    if (t >= ntiles) return;
+    const int nk = a.kp / 64;
+    const unsigned lds0 = (unsigned)(unsigned long long)smem;
+    const int lrow = lane >> 3, lchunk = (lane & 7) ^ (lrow & 7);
+
+    const int c0 = t * 256;
+    const long long arows = min(256, a.cout - c0);
+    const i32x4_t rsA = make_rsrc((const char*)a.w + (long long)c0 * a.kp * ESZ, (unsigned)(arows * a.kp * ESZ));
+    const i32x4_t rsB = make_rsrc(a.x, (unsigned)((long long)a.P * a.cin * ESZ));
+    unsigned a_off[2][2], b_off[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int row = h * 128 + (wave + 8 * i) * 8 + lrow;
+            a_off[h][i] = row < arows ? (unsigned)(((long long)row * a.kp + lchunk * VEC) * ESZ) : OOB;
+        }
+        const int p = (wave + 8 * i) * 8 + lrow;
+        b_off[i] = p < a.P ? (unsigned)(((long long)p * a.cin + lchunk * VEC) * ESZ) : OOB;
+    }
+    // half-tile X (0 A0, 1 A1, 2 B0) of K-step kt into its ring stage; K-steps >= nk load zeros
+    auto issue = [&](int X, int kt) {
+        const unsigned dst = lds0 + (kt % 3) * ST + X * HT;
+        const bool live = kt < nk;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const unsigned base = X < 2 ? a_off[X][i] : b_off[i];
+            const unsigned off = (live && base != OOB) ? base + (unsigned)(kt * 128) : OOB;
+            dma16(X < 2 ? rsA : rsB, off, dst + (wave + 8 * i) * 1024);
+        }
+    };
+
+    f32x4_t acc[2][4][2];
+#pragma unroll
+    for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[qa][i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    const int r16 = lane & 15, kq = lane >> 4;
+    uint4 fa[4][2], fb[2][2];
+    auto read_a = [&](int kt, int h) {
+        const char* base = smem + (kt % 3) * ST + h * HT;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int hs = 0; hs < 2; ++hs)
+                fa[i][hs] = *reinterpret_cast<const uint4*>(base + swz(grp * 64 + i * 16 + r16, kq + 4 * hs));
+    };
+    auto read_b = [&](int kt) {
+        const char* base = smem + (kt % 3) * ST + 2 * HT;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int hs = 0; hs < 2; ++hs)
+                fb[j][hs] = *reinterpret_cast<const uint4*>(base + swz(wn * 32 + j * 16 + r16, kq + 4 * hs));
+    };
+    auto mfma_q = [&](int qa) {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int hs = 0; hs < 2; ++hs)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    if constexpr (std::is_same<T, f16_t>::value)
+                        acc[qa][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                            __builtin_bit_cast(f16x8_t, fa[i][hs]), __builtin_bit_cast(f16x8_t, fb[j][hs]),
+                            acc[qa][i][j], 0, 0, 0);
+                    else
+                        acc[qa][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                            __builtin_bit_cast(bf16x8_t, fa[i][hs]), __builtin_bit_cast(bf16x8_t, fb[j][hs]),
+                            acc[qa][i][j], 0, 0, 0);
+                }
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto bar = []() { asm volatile("s_barrier" ::: "memory"); };
+
+    // prologue: K-steps 0 and 1 (A0, B0, A1 each); K-step 0's A0 / B0 landed
+    issue(0, 0); issue(2, 0); issue(1, 0);
+    issue(0, 1); issue(2, 1); issue(1, 1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    bar();
+    if (grp == 1) bar();  // stagger: group 1 runs one barrier behind group 0
+    for (int kt = 0; kt < nk; ++kt) {
+        // phase A: A0 x B0 of K-step kt; K-step kt + 2's A0 / B0 into the stage kt - 1 used
+        read_a(kt, 0); read_b(kt);
+        issue(0, kt + 2); issue(2, kt + 2);
+        asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // K-step kt's A1 has landed
+        bar(); mfma_q(0); bar();
+        // phase B: A1 x B0 (B fragments from registers); K-step kt + 2's A1
+        read_a(kt, 1);
+        issue(1, kt + 2);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // K-step kt + 1's A0 / B0 have landed
+        bar(); mfma_q(1); bar();
+    }
+    if (grp == 0) bar();  // equal barrier counts: every wave's LDS reads are done
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    // ---- epilogue: scores (database row c, query p) -> kNN screen or the f32 slab
+    float* __restrict__ Y = (float*)a.y;
+#pragma unroll
+    for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int c = c0 + qa * 128 + grp * 64 + i * 16 + 4 * kq;
+            if (c >= a.cout) continue;
+            const bool full = c + 3 < a.cout;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int p = wn * 32 + j * 16 + r16;
+                if (p >= a.P) continue;
+                float v[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = acc[qa][i][j][r];
+                if (a.scr_k) {  // kNN screen: append survivors, store nothing
+                    screen_append(a, v, c, a.cout, p, a.scr_tau[p]);
+                    continue;
+                }
+                const long long o = (long long)p * a.ldy + c;
+                if (full) {
+                    St4<float>::st(Y + o, v);
+                } else {
+                    for (int r = 0; r < 4; ++r)
+                        if (c + r < a.cout) Y[o + r] = v[r];
+                }
+            }
+        }
+}
+
 static int g_gemm8 = -1;  // rr_set_tuning(RR_TUNE_GEMM8) / RR_GEMM8: 0 off, 1 auto (default), 2 force where legal
 static bool g_gemm8_tile = false;  // RR_TUNE_GEMM8 value | 4: one block per tile instead of persistent blocks
 
@@ -1003,6 +1161,26 @@ static bool try_gemm8(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
     }
 }
 
+static int g_gemm8h = 1;  // rr_set_tuning(RR_TUNE_GEMM8, value | 8): k_gemm8h off
+
+// k_gemm8h: 16-bit 1x1 score GEMM (float out, natural row order, no affine /
+// residual / activation) with <= 128 "pixels" (queries), long channel dim.
+template <typename T, typename TO>
+static bool try_gemm8h(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
+    if constexpr (sizeof(T) != 2 || !std::is_same<TO, float>::value) {
+        return false;
+    } else {
+        if (!g_gemm8h || !k1 || perm || a.kp % 64 || a.kp != a.cin || a.kp / 64 < 2) return false;
+        if (a.flags & (RR_CONV_AFFINE | RR_CONV_RESIDUAL) || a.act != RR_ACT_IDENTITY) return false;
+        if (a.P < 1 || a.P > 128 || (long long)a.P * a.cin * 2 >= (1ll << 31) || 256ll * a.kp * 2 >= (1ll << 31))
+            return false;
+        const long long ntiles = ((long long)a.cout + 255) / 256;
+        if (ntiles >= (1ll << 31)) return false;
+        hipLaunchKernelGGL((k_gemm8h<T>), dim3((unsigned)ntiles), dim3(512), 0, s, a, (int)ntiles);
+        return true;
+    }
+}
+
 int g_force_cfg = 0;  // rr_set_tuning(RR_TUNE_GEMM_CONFIG, ...)
 
 template <typename T, typename TO>
@@ -1038,6 +1216,8 @@ void launch_gemm2(const ConvArgs& a, bool k1, hipStream_t s) {
         launch_cfg3<T, TO, 256, 32, 4, 1>(a, k1, perm, s);
     else if (a.P <= 64)
         launch_cfg3<T, TO, 256, 64, 4, 1>(a, k1, perm, s);
+    else if (a.P <= 128 && a.cout >= 4096 && try_gemm8h<T, TO>(a, k1, perm, s))  // kNN score GEMM at 65..128 queries
+        return;
     else if (a.P <= 128 && a.cout >= 4096)  // kNN score GEMM at 65..128 queries: no half-empty 256-wide pixel tiles;
         // 128 x 128 (4 waves, 64 KiB: two blocks per CU) measured 1.296 / 1.306 vs 1.328 / 1.335 ms for the
         // Q = 128 search against 1M x 2048 with 256 x 128 (tools/knn_cfg_ab.sh)
@@ -1064,6 +1244,7 @@ void set_gemm_tuning(int key, int value) {
     else if (key == RR_TUNE_GEMM_ASTAT) g_ast = value != 0;
     else if (key == RR_TUNE_GEMM_XCD_MAP) g_xmap = value != 0;
     else if (key == RR_TUNE_GEMM8) {
+        g_gemm8h = !(value >= 0 && (value & 8));
         g_gemm8_tile = value >= 0 && (value & 4);
         value = value < 0 ? 0 : value & 3;
         g_gemm8 = value > 2 ? 2 : value;

@@ -281,3 +281,27 @@ def test_knn_verify_tight_cluster(cuda, prec):
     assert unc[0] == 0 and unc[1] == 0 and unc[3] == 0
     if prec != "fp32":
         assert unc[2] == 1
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+@pytest.mark.parametrize("nq", [1, 37, 128])
+def test_knn_half_width_gemm_equals_tiled(cuda, prec, nq):
+    """<= 128 queries: the score GEMM on k_gemm8h (256 database rows x 128
+    queries, 8-phase staggered, 3-stage ring) vs the tiled engine
+    (rr_set_tuning(RR_TUNE_GEMM8, 1 | 8)): identical top-k indices and exact
+    float64 scores, over the prefix slab and the fused screen (n = 300k rows,
+    a ragged last database tile)."""
+    from cirtorch import _engine as E
+    from cirtorch import _ops
+    from cirtorch.search import KnnIndex
+    db = _ops.fill_unit_rows(300_001, 2048, seed=0x5EED8, device=cuda)
+    q = _ops.fill_unit_rows(nq, 2048, seed=0x5EED9 + nq, device=cuda)
+    out = {}
+    try:
+        for v in (1, 9):
+            E.check(E.lib().rr_set_tuning(8, v), "rr_set_tuning")
+            out[v] = KnnIndex(db, prec).search(q, 100)
+    finally:
+        E.lib().rr_set_tuning(8, 1)
+    assert torch.equal(out[1][1], out[9][1])
+    assert torch.equal(out[1][0], out[9][0])
