@@ -1102,6 +1102,220 @@ __global__ void __launch_bounds__(512, 1) k_gemm8h(ConvArgs a, int ntiles) {
         }
 }
 
+// ---------------------------------------------------------------------------
+// The mirror of k_gemm8h for 128-channel convs (auto: the strided mod3 3x3,
+// 699 vs 775 us on k_igemm at 128 images; the stride-1 mod3 3x3 stays on the
+// direct k_conv3x3, 550 vs 664 us on this kernel):
+// a 128 (output channels, A) x 256 (pixels, B) tile, phases A0 x B0 and
+// A0 x B1 (the A fragments stay in registers for the second), the same
+// 3-stage {A0, B0, B1} ring / issue distances / counted waits, k_gemm8's
+// operand-B addressing (1x1 or tap-uniform im2col) and PERM32 epilogue
+// (folded BN, residual, activation, one 16-B store per fragment pair).
+template <typename T, int KM>
+__global__ void __launch_bounds__(512, 1) k_gemm8a(ConvArgs a, int tiles_p, int ntiles) {
+    static_assert(sizeof(T) == 2, "16-bit operands");
+    constexpr bool K1 = KM == 1, tapu = KM == 2;
+    constexpr int VEC = 8, ESZ = 2, HT = 16384, ST = 3 * HT;  // stage = [A0, B0, B1]
+    __shared__ __attribute__((aligned(1024))) char smem[3 * ST];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wave >> 2, wn = wave & 3;
+    const int bx = (int)blockIdx.x, xcd = bx & 7;
+    const int nt8 = ntiles >> 3, rt8 = ntiles & 7;
+    const int t = (xcd < rt8 ? xcd * (nt8 + 1) : rt8 * (nt8 + 1) + (xcd - rt8) * nt8) + (bx >> 3);
+    if (t >= ntiles) return;
+    const int H = a.h, W = a.w_, Cin = a.cin;
+    const int nk = a.kp / 64;
+    const unsigned lds0 = (unsigned)(unsigned long long)smem;
+    const int lrow = lane >> 3, lchunk = (lane & 7) ^ (lrow & 7);
+
+    const int c0 = (t / tiles_p) * 128, p0 = (t % tiles_p) * 256;
+    const long long arows = min(128, a.cout - c0);
+    const i32x4_t rsA = make_rsrc((const char*)a.w + (long long)c0 * a.kp * ESZ, (unsigned)(arows * a.kp * ESZ));
+    const i32x4_t rsB = make_rsrc(a.x, (unsigned)((long long)a.n * H * W * Cin * ESZ));
+    unsigned a_off[2], b_base[2][2];
+    int b_hi[2][2], b_wi[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int arow = (wave + 8 * i) * 8 + lrow;
+        a_off[i] = arow < arows ? (unsigned)(((long long)arow * a.kp + lchunk * VEC) * ESZ) : OOB;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int p = p0 + h * 128 + (wave + 8 * i) * 8 + lrow;
+            if (p < a.P) {
+                const int img = p / (a.ho * a.wo);
+                const int rem = p - img * (a.ho * a.wo);
+                const int oh = rem / a.wo, ow = rem - oh * a.wo;
+                b_hi[h][i] = oh * a.stride - a.pad;
+                b_wi[h][i] = ow * a.stride - a.pad;
+                b_base[h][i] = (unsigned)((long long)img * H * W * Cin +
+                                          ((long long)b_hi[h][i] * W + b_wi[h][i]) * Cin + lchunk * VEC);
+            } else {
+                b_hi[h][i] = b_wi[h][i] = -(1 << 28);
+                b_base[h][i] = OOB;
+            }
+        }
+    }
+    // half-tile X (0 A0, 1 B0, 2 B1) of K-step kt into its ring stage; K-steps >= nk load zeros
+    auto issue = [&](int X, int kt) {
+        const unsigned dst = lds0 + (kt % 3) * ST + X * HT;
+        const bool live = kt < nk;
+        if (X == 0) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const unsigned off = (live && a_off[i] != OOB) ? a_off[i] + (unsigned)(kt * 128) : OOB;
+                dma16(rsA, off, dst + (wave + 8 * i) * 1024);
+            }
+        } else {
+            const int h = X - 1, k0 = kt * 64;
+            int tap_dh = 0, tap_dw = 0, tap_add = 0;
+            if constexpr (tapu) {
+                const int tap = k0 >> a.lc, ci0 = k0 & (Cin - 1);
+                const int kh = tap / a.kw, kw = tap - kh * a.kw;
+                tap_dh = kh * a.dil;
+                tap_dw = kw * a.dil;
+                tap_add = (tap_dh * W + tap_dw) * Cin + ci0;
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                unsigned off = OOB;
+                if (live && b_base[h][i] != OOB) {
+                    if constexpr (K1) {
+                        off = (b_base[h][i] + (unsigned)k0) * ESZ;
+                    } else {
+                        const int hi = b_hi[h][i] + tap_dh, wi = b_wi[h][i] + tap_dw;
+                        if ((unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W)
+                            off = (b_base[h][i] + (unsigned)tap_add) * ESZ;
+                    }
+                }
+                dma16(rsB, off, dst + (wave + 8 * i) * 1024);
+            }
+        }
+    };
+
+    f32x4_t acc[2][4][2];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[qb][i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    const int r16 = lane & 15, kq = lane >> 4;
+    uint4 fa[4][2], fb[2][2];
+    auto read_a = [&](int kt) {
+        const char* base = smem + (kt % 3) * ST;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int hs = 0; hs < 2; ++hs)
+                fa[i][hs] = *reinterpret_cast<const uint4*>(base + swz(grp * 64 + i * 16 + r16, kq + 4 * hs));
+    };
+    auto read_b = [&](int kt, int h) {
+        const char* base = smem + (kt % 3) * ST + (1 + h) * HT;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int hs = 0; hs < 2; ++hs)
+                fb[j][hs] = *reinterpret_cast<const uint4*>(base + swz(wn * 32 + j * 16 + r16, kq + 4 * hs));
+    };
+    auto mfma_q = [&](int qb) {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int hs = 0; hs < 2; ++hs)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    if constexpr (std::is_same<T, f16_t>::value)
+                        acc[qb][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                            __builtin_bit_cast(f16x8_t, fa[i][hs]), __builtin_bit_cast(f16x8_t, fb[j][hs]),
+                            acc[qb][i][j], 0, 0, 0);
+                    else
+                        acc[qb][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                            __builtin_bit_cast(bf16x8_t, fa[i][hs]), __builtin_bit_cast(bf16x8_t, fb[j][hs]),
+                            acc[qb][i][j], 0, 0, 0);
+                }
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto bar = []() { asm volatile("s_barrier" ::: "memory"); };
+
+    issue(0, 0); issue(1, 0); issue(2, 0);
+    issue(0, 1); issue(1, 1); issue(2, 1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // K-step 0's A0 / B0
+    bar();
+    if (grp == 1) bar();
+    for (int kt = 0; kt < nk; ++kt) {
+        // phase A: A0 x B0 of K-step kt; K-step kt + 2's A0 / B0
+        read_a(kt); read_b(kt, 0);
+        issue(0, kt + 2); issue(1, kt + 2);
+        asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // K-step kt's B1 has landed
+        bar(); mfma_q(0); bar();
+        // phase B: A0 (registers) x B1; K-step kt + 2's B1
+        read_b(kt, 1);
+        issue(2, kt + 2);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // K-step kt + 1's A0 / B0 have landed
+        bar(); mfma_q(1); bar();
+    }
+    if (grp == 0) bar();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    // ---- epilogue (PERM32 rows): folded BN scale / shift, residual, activation, NHWC store
+    T* __restrict__ Y = (T*)a.y;
+    const T* __restrict__ R = (const T*)a.res;
+    const bool affine = a.flags & RR_CONV_AFFINE;
+    const bool resid = a.flags & RR_CONV_RESIDUAL;
+    const bool leaky = a.act == RR_ACT_LEAKY;
+#pragma unroll
+    for (int i2 = 0; i2 < 2; ++i2) {
+        const int c = c0 + grp * 64 + 32 * i2 + 8 * kq;  // 8 consecutive channels
+        if (c >= a.cout) continue;
+        float sc[8], sh[8];
+        if (affine) {
+            St4<float>::ld(a.scale + c, sc);
+            St4<float>::ld(a.scale + c + 4, sc + 4);
+            St4<float>::ld(a.shift + c, sh);
+            St4<float>::ld(a.shift + c + 4, sh + 4);
+        } else {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) { sc[r] = 1.f; sh[r] = 0.f; }
+        }
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int p = p0 + qb * 128 + wn * 32 + j * 16 + r16;
+                if (p >= a.P) continue;
+                float v[8];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    v[r] = acc[qb][2 * i2][j][r] * sc[r] + sh[r];
+                    v[4 + r] = acc[qb][2 * i2 + 1][j][r] * sc[4 + r] + sh[4 + r];
+                }
+                const long long o = (long long)p * a.ldy + c;
+                if (resid) {
+                    float rv[8];
+                    St4<T>::ld(R + o, rv);
+                    St4<T>::ld(R + o + 4, rv + 4);
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) v[r] += rv[r];
+                }
+                if (leaky) {
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * a.slope;
+                }
+                uint4 q;
+                q.x = H16<T>::pack2(v[0], v[1]);
+                q.y = H16<T>::pack2(v[2], v[3]);
+                q.z = H16<T>::pack2(v[4], v[5]);
+                q.w = H16<T>::pack2(v[6], v[7]);
+                *reinterpret_cast<uint4*>(Y + o) = q;
+            }
+    }
+}
+
 static int g_gemm8 = -1;  // rr_set_tuning(RR_TUNE_GEMM8) / RR_GEMM8: 0 off, 1 auto (default), 2 force where legal
 static bool g_gemm8_tile = false;  // RR_TUNE_GEMM8 value | 4: one block per tile instead of persistent blocks
 
@@ -1181,6 +1395,33 @@ static bool try_gemm8h(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
     }
 }
 
+static int g_gemm8a = 1;  // rr_set_tuning(RR_TUNE_GEMM8, value | 16): k_gemm8a off
+
+// k_gemm8a: 16-bit PERM32 convs with 128-multiple c_out below 256 (1x1 or
+// tap-uniform im2col), enough 128 x 256 tiles to fill the chip twice.
+bool gemm8a_eligible(const ConvArgs& a, bool k1) {
+    if (!g_gemm8a || !(a.flags & RR_CONV_PERM32) || a.cout % 128 || a.cout >= 256) return false;
+    const int km = k1 ? 1 : (a.cin * 2) % 128 == 0 ? 2 : 0;
+    if (km == 0 || a.kp % 64 || a.kp / 64 < 2) return false;
+    if ((long long)a.n * a.h * a.w_ * a.cin * 2 >= (1ll << 31) || 128ll * a.kp * 2 >= (1ll << 31)) return false;
+    const long long ntiles = (long long)((a.P + 255) / 256) * (a.cout / 128);
+    return ntiles >= 2 * grid_cus() && ntiles < (1ll << 31);
+}
+
+template <typename T, typename TO>
+static bool try_gemm8a(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
+    if constexpr (sizeof(T) != 2 || !std::is_same<T, TO>::value) {
+        return false;
+    } else {
+        if (!perm || !gemm8a_eligible(a, k1)) return false;
+        const int tiles_p = (a.P + 255) / 256;
+        const int ntiles = tiles_p * (a.cout / 128);
+        if (k1) hipLaunchKernelGGL((k_gemm8a<T, 1>), dim3(ntiles), dim3(512), 0, s, a, tiles_p, ntiles);
+        else hipLaunchKernelGGL((k_gemm8a<T, 2>), dim3(ntiles), dim3(512), 0, s, a, tiles_p, ntiles);
+        return true;
+    }
+}
+
 int g_force_cfg = 0;  // rr_set_tuning(RR_TUNE_GEMM_CONFIG, ...)
 
 template <typename T, typename TO>
@@ -1199,6 +1440,7 @@ void launch_gemm2(const ConvArgs& a, bool k1, hipStream_t s) {
         default: break;
     }
     if (g_force_cfg == 0 && try_gemm8<T, TO>(a, k1, perm, s)) return;
+    if (g_force_cfg == 0 && try_gemm8a<T, TO>(a, k1, perm, s)) return;
     // A-stationary variants (single output-channel tile, short K)
     const int nk = a.kp / (sizeof(T) == 2 ? 64 : 32);
     if (g_force_cfg == 6 || (g_force_cfg == 0 && g_ast)) {
@@ -1245,6 +1487,7 @@ void set_gemm_tuning(int key, int value) {
     else if (key == RR_TUNE_GEMM_XCD_MAP) g_xmap = value != 0;
     else if (key == RR_TUNE_GEMM8) {
         g_gemm8h = !(value >= 0 && (value & 8));
+        g_gemm8a = !(value >= 0 && (value & 16));
         g_gemm8_tile = value >= 0 && (value & 4);
         value = value < 0 ? 0 : value & 3;
         g_gemm8 = value > 2 ? 2 : value;

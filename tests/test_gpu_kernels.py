@@ -675,3 +675,39 @@ def test_gemm8_persistent_equals_one_block_per_tile(cuda, shape, cap):
         E.lib().rr_set_tuning(5, 1)
     assert torch.equal(got, ref)
 
+
+
+@pytest.mark.parametrize("shape", [(8, 128, 128, 128, 128, 3, 1), (32, 128, 128, 128, 128, 3, 2),
+                                   (11, 100, 124, 128, 128, 3, 1)])
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_gemm8a_bit_identical_to_tiled_engine(cuda, shape, prec):
+    """128-channel 3x3 convs (mod3 shapes at >= 512 tiles, stride 1 and 2, a
+    ragged last pixel tile) on k_gemm8a (128 channels x 256 pixels, 8-phase,
+    3-stage ring) vs the tiled engine (RR_TUNE_GEMM8 | 16): same operand
+    layout and K order, bit-identical; and against float64 within the 16-bit
+    tolerance."""
+    from cirtorch import _engine as E
+    n, h, w, cin, cout, k, s = shape
+    g = torch.Generator(device=cuda).manual_seed(17)
+    dt = torch.bfloat16 if prec == "bf16" else torch.float16
+    x = torch.randn((n, h, w, cin), generator=g, device=cuda).to(dt)
+    wt = torch.randn((cout, cin, k, k), generator=g, device=cuda) * (2.0 / (cin * k * k)) ** 0.5
+    wp = _ops().pack_conv_weights(wt, cin, dt, perm32=True)
+    sc = torch.rand(cout, generator=g, device=cuda) + 0.5
+    sh = torch.randn(cout, generator=g, device=cuda) * 0.1
+    E.check(E.lib().rr_set_tuning(6, 0), "rr_set_tuning")
+    E.check(E.lib().rr_set_tuning(5, 0), "rr_set_tuning")
+    try:
+        a = _ops().conv2d_fused(x, wp, k, k, s, 1, cout, sc, sh, leaky=True, perm32=True)
+        E.check(E.lib().rr_set_tuning(8, 1 | 16), "rr_set_tuning")
+        b = _ops().conv2d_fused(x, wp, k, k, s, 1, cout, sc, sh, leaky=True, perm32=True)
+    finally:
+        E.lib().rr_set_tuning(8, 1)
+        E.lib().rr_set_tuning(6, 1)
+        E.lib().rr_set_tuning(5, 1)
+    assert torch.equal(a, b)
+    ref = F.conv2d(x[:1].cpu().permute(0, 3, 1, 2).double(), wt.to(dt).cpu().double(), stride=s, padding=1)
+    ref = ref * sc.cpu().double()[None, :, None, None] + sh.cpu().double()[None, :, None, None]
+    ref = F.leaky_relu(ref, 0.01).permute(0, 2, 3, 1)
+    err = (a[:1].cpu().double() - ref).abs().max().item()
+    assert err <= 2e-2 * ref.abs().max().item(), err
