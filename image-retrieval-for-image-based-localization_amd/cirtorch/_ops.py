@@ -267,6 +267,14 @@ def whitenapply_rows(x, m, P, d_out):
     m = m.contiguous().double().reshape(-1)
     P = P.contiguous().double()
     rows, dim = x.shape
+    if dim % 16:
+        # the f64 MFMA kernel takes 16-wide K-steps: zero columns of x, m and P
+        # add exact zeros to every dot product (any D, like the numpy reference)
+        pad = 16 - dim % 16
+        x = torch.nn.functional.pad(x, (0, pad))
+        m = torch.nn.functional.pad(m, (0, pad))
+        P = torch.nn.functional.pad(P, (0, pad))
+        dim += pad
     y = torch.empty((rows, d_out), dtype=torch.float32, device=x.device)
     ws = torch.empty(max(1, int(E.lib().rr_whiten_workspace_bytes(rows, d_out))), dtype=torch.uint8, device=x.device)
     E.check(E.lib().rr_whitenapply(E.ptr(x), rows, dim, E.ptr(m), E.ptr(P), int(d_out), E.ptr(y), E.ptr(ws),

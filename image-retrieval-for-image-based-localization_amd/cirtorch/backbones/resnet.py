@@ -30,7 +30,7 @@ import torch.nn.functional as F
 
 from .. import _ops
 from ..modules.abn import ABN
-from .misc import ResidualBlock
+from .misc import ResidualBlock, make_step, run_step
 
 CONV_PARAMS = ["weight"]
 BN_PARAMS = ["weight", "bias", "running_mean", "running_var"]
@@ -44,10 +44,6 @@ def try_index(scalar_or_list, i):
         return scalar_or_list[i]
     except TypeError:
         return scalar_or_list
-
-
-class _ConvStep:
-    __slots__ = ("w", "kh", "kw", "stride", "pad", "c_out", "scale", "shift", "leaky", "slope", "perm")
 
 
 class ResNet(nn.Module):
@@ -97,8 +93,7 @@ class ResNet(nn.Module):
             self.add_module("mod%d" % (mod_id + 2), nn.Sequential(OrderedDict(blocks)))
             channels = [c * 2 for c in channels]
         self.out_channels = in_channels
-        self.engine_dtype = _PRECISIONS[precision]
-        self._plan = None
+        self.set_precision(precision)
 
     # ------------------------------------------------------------ reference API
     @staticmethod
@@ -138,6 +133,9 @@ class ResNet(nn.Module):
     # ------------------------------------------------------------ engine plan
     def set_precision(self, precision):
         self.engine_dtype = _PRECISIONS[precision]
+        for m in self.modules():
+            if isinstance(m, ResidualBlock):
+                m.engine_dtype = self.engine_dtype  # standalone block calls run in the body's precision
         self._plan = None
         return self
 
@@ -157,22 +155,7 @@ class ResNet(nn.Module):
         return 4 if self.engine_dtype == torch.float32 else 8
 
     def _step(self, conv, bn, cin_pad=None, leaky_override=None):
-        st = _ConvStep()
-        co, ci, kh, kw = conv.weight.shape
-        cin_pad = cin_pad or ci
-        # engine layout [c_out][(kh*KW + kw)*c_in + ci], 128-B K-steps, rows in the
-        # 32-row MFMA-interleaved order so each lane stores 8 consecutive channels
-        st.perm = co % 32 == 0
-        st.w = _ops.pack_conv_weights(conv.weight, cin_pad, self.engine_dtype, perm32=st.perm)
-        st.kh, st.kw = kh, kw
-        st.stride = conv.stride[0]
-        st.pad = conv.padding[0]
-        st.c_out = co
-        st.scale, st.shift = bn.folded()
-        st.leaky, st.slope = bn.slope()
-        if leaky_override is not None:
-            st.leaky = leaky_override
-        return st
+        return make_step(conv, bn, self.engine_dtype, cin_pad=cin_pad, leaky_override=leaky_override)
 
     def _build_plan(self):
         dev = self.mod1.conv1.weight.device
@@ -188,23 +171,14 @@ class ResNet(nn.Module):
             mod = getattr(self, "mod%d" % (mod_id + 2))
             blocks = []
             for blk in mod.children():
-                c = blk.convs
-                post_leaky, post_slope = c.bn1.slope()  # post-add activation (misc.py:194-203)
-                if blk.is_bottleneck:
-                    steps = [self._step(c.conv1, c.bn1), self._step(c.conv2, c.bn2), self._step(c.conv3, c.bn3)]
-                else:
-                    steps = [self._step(c.conv1, c.bn1), self._step(c.conv2, c.bn2)]
-                steps[-1].leaky, steps[-1].slope = post_leaky, post_slope
-                proj = self._step(blk.proj_conv, blk.proj_bn, leaky_override=False) if hasattr(blk, "proj_conv") else None
-                blocks.append((steps, proj))
+                blocks.append(blk.engine_plan(self.engine_dtype))
             plan["mods"].append(blocks)
         self._plan = plan
         return plan
 
     @staticmethod
     def _conv(t, st, residual=None):
-        return _ops.conv2d_fused(t, st.w, st.kh, st.kw, st.stride, st.pad, st.c_out, st.scale, st.shift,
-                                 residual=residual, leaky=st.leaky, slope=st.slope, perm32=st.perm)
+        return run_step(t, st, residual)
 
     def forward(self, x, normalize=None):
         """x: [N, 3, H, W] float32 on the GPU, or uint8 pixels (read as x / 255) (already normalised unless

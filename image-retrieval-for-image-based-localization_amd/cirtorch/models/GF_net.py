@@ -26,7 +26,7 @@ from ..modules.heads.global_head import globalHead
 from ..utils.parallel import PackedSequence
 from ..utils.sequence import pad_packed_images
 
-OUTPUT_DIM = {"resnet18": 512, "resnet34": 512, "resnet50": 2048, "resnet101": 2048, "resnet152": 2048}
+from ..modules.utils import OUTPUT_DIM  # noqa: E402  (reference cirtorch/modules/utils.py:61-79)
 
 
 class Normalize:
@@ -104,7 +104,7 @@ class ImageRetrievalNet(nn.Module):
                 preds.append(pred["ret_pred"].unsqueeze(0))
             pred = torch.cat(preds, dim=0).permute(1, 2, 0)
             pred = nn.functional.avg_pool1d(pred, kernel_size=len(scales)).squeeze(-1)
-            return None, OrderedDict([("ret_pred", pred)])
+            return OrderedDict([("ret_loss", None)]), OrderedDict([("ret_pred", pred)])
         if isinstance(img, torch.Tensor):
             if img.dtype == torch.uint8:  # pixels -> [0, 1] (to_tensor) for the resize / padding paths
                 img = _ops.pixels_to_unit(img)
@@ -116,7 +116,7 @@ class ImageRetrievalNet(nn.Module):
                 preds.append(pred["ret_pred"].unsqueeze(0))
             pred = torch.cat(preds, dim=0).permute(1, 2, 0)
             pred = nn.functional.avg_pool1d(pred, kernel_size=len(scales)).squeeze(-1)
-            return None, OrderedDict([("ret_pred", pred)])
+            return OrderedDict([("ret_loss", None)]), OrderedDict([("ret_pred", pred)])
 
         padded, valid_size = pad_packed_images(img)
         x = self.body(padded, normalize=self._normalizer())
@@ -168,8 +168,9 @@ def init_network(params):
     mean = params.get("mean", [0.485, 0.456, 0.406])
     std = params.get("std", [0.229, 0.224, 0.225])
     # fp16 by default: it meets the north_star descriptor bar (cosine >= 1 - 1e-4
-    # vs the fp32 reference) at bf16 speed; "bf16" is an explicit opt-in and
-    # "fp32" the exact-f32 MFMA parity mode.
+    # vs the fp32 reference) at bf16 speed; extract_vectors re-extracts any
+    # descriptor that overflowed fp16's range in bf16.  "bf16" is an explicit
+    # opt-in and "fp32" the exact-f32 MFMA parity mode.
     return make_net(arch, pooling, params.get("whitening", False), mean, std,
                     precision=params.get("precision", "fp16"))
 
@@ -263,18 +264,22 @@ def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], 
     def run(part, items):
         """one same-size group of images -> their descriptor columns"""
         slot = state["slot"]
-        if len(part) > 1:
+        if items[0].is_cuda:                  # device tensors: stacked in place, no host staging
+            x = torch.stack([t.to(dev) for t in items]) if len(items) > 1 else items[0].to(dev)[None]
+            host = None
+        elif len(part) > 1:
             copied[slot].synchronize()        # the previous H2D out of this slot's host buffer has finished
             host = _pinned_chain(slot, (len(part),) + tuple(items[0].shape), items[0].dtype)
             torch.stack(items, out=host)      # (measured: faster than a per-image copy on 8 host threads)
         else:
             host = items[0][None]
-        copy.wait_event(freed[slot])          # the extractor is done with this slot's device buffer
-        with torch.cuda.stream(copy):
-            x = host.to(dev, non_blocking=len(part) > 1)
-        copied[slot].record(copy)
-        main.wait_event(copied[slot])
-        x.record_stream(main)
+        if host is not None:
+            copy.wait_event(freed[slot])      # the extractor is done with this slot's device buffer
+            with torch.cuda.stream(copy):
+                x = host.to(dev, non_blocking=len(part) > 1)
+            copied[slot].record(copy)
+            main.wait_event(copied[slot])
+            x.record_stream(main)
         if x.dtype == torch.uint8 and (ms != [1] or not normalize_in_net):
             x = _ops.pixels_to_unit(x)
         elif x.dtype != torch.uint8:
@@ -322,4 +327,22 @@ def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], 
                 vecs[:, cols] = torch.cat([v for _, v in outs], dim=1)
     finally:
         net.augment = saved
-    return vecs.cpu()
+    out = vecs.cpu()
+    # fp16 activations saturate at 65504: a descriptor that overflowed (checkpoints
+    # whose activations leave fp16 range) is re-extracted with bf16 storage (fp32
+    # range) instead of being returned as inf / NaN.  One check on the host copy.
+    body = getattr(net, "body", None)
+    bad = (~torch.isfinite(out)).any(dim=0).nonzero().flatten().tolist()
+    if bad and getattr(body, "engine_dtype", None) == torch.float16 and hasattr(body, "set_precision"):
+        import warnings
+        warnings.warn("extract_vectors: %d descriptor(s) overflowed fp16; re-extracting them in bf16" % len(bad))
+        body.set_precision("bf16")
+        try:
+            redo = extract_vectors(net, [images[i] for i in bad], image_size, transform=transform,
+                                   bbxs=[bbxs[i] for i in bad] if bbxs is not None else None, ms=ms, msp=msp,
+                                   print_freq=print_freq, batch=batch, workers=workers,
+                                   test_transform=test_transform)
+        finally:
+            body.set_precision("fp16")
+        out[:, bad] = redo
+    return out

@@ -65,3 +65,6 @@ class ABN(nn.Module):
 
 InPlaceABN = ABN
 InPlaceABNSync = ABN
+# reference cirtorch/utils/misc.py:48-86: "drop-in replacement for ABN which performs
+# inference-mode BN + activation" -- exactly the folded epilogue above
+ActivatedAffine = ABN

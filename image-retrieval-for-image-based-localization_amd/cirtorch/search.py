@@ -95,10 +95,10 @@ class KnnIndex:
         near-duplicates tighter than the bf16 / fp16 screening error — with
         float32 screening and more candidates; this costs one device->host
         read per search (no graph capture)."""
-        if verify:
-            return self._search_verified(q_rows, k)
         if q_rows.shape[1] != self.dim:
             raise RuntimeError("KnnIndex.search: queries have D=%d, the database D=%d" % (q_rows.shape[1], self.dim))
+        if verify:
+            return self._search_verified(q_rows, k)
         q32 = _pad_cols(q_rows.float().contiguous(), self.d_pad)
         if self.ntotal == 0 or q32.shape[0] == 0:
             s = torch.full((q32.shape[0], k), float("-inf"), dtype=torch.float64, device=q32.device)

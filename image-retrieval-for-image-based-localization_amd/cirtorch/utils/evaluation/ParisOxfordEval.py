@@ -27,20 +27,24 @@ except ImportError:  # pragma: no cover
 
 def _positions(ranks):
     """ranks [N_ranked, Q] (numpy or torch) -> posof [Q, N_db] int64 with the rank
-    position of each database item (-1 where an item is not in the list)."""
+    position of each database item (-1 where an item is not in the list).
+    Negative entries (the -1 fill of unfilled kNN slots, k > N) are ignored:
+    they scatter into a dummy column that is dropped."""
     if torch is not None and torch.is_tensor(ranks):
         r = ranks.long()
         n, q = r.shape
-        ndb = int(r.max().item()) + 1 if r.numel() else 0
-        pos = torch.full((q, ndb), -1, dtype=torch.int64, device=r.device)
+        ndb = max(int(r.max().item()) + 1, 0) if r.numel() else 0
+        r = torch.where(r < 0, torch.full_like(r, ndb), r)
+        pos = torch.full((q, ndb + 1), -1, dtype=torch.int64, device=r.device)
         pos.scatter_(1, r.t().contiguous(), torch.arange(n, device=r.device).expand(q, n).contiguous())
-        return pos.cpu().numpy()
+        return pos[:, :ndb].cpu().numpy()
     r = np.asarray(ranks).astype(np.int64, copy=False)
     n, q = r.shape
-    ndb = int(r.max()) + 1 if r.size else 0
-    pos = np.full((q, ndb), -1, dtype=np.int64)
+    ndb = max(int(r.max()) + 1, 0) if r.size else 0
+    r = np.where(r < 0, ndb, r)
+    pos = np.full((q, ndb + 1), -1, dtype=np.int64)
     pos[np.arange(q)[:, None], r.T] = np.arange(n)[None, :]
-    return pos
+    return pos[:, :ndb]
 
 
 def _ranked(posq, items):

@@ -468,9 +468,12 @@ int g_conv3_mode = 1;  // rr_set_tuning(RR_TUNE_CONV3X3): 0 off, 1 auto, 2 / 3 p
 // image sizes the tiles divide; returns false otherwise (caller falls back to
 // the implicit-GEMM engine).
 bool gemm8_eligible(const ConvArgs& a, bool k1, int esz);  // rr_gemm.hip
+bool launch_conv3s(const ConvArgs& a, hipStream_t s, bool f16);  // rr_conv3s.hip
 
 bool launch_conv3x3(const ConvArgs& a, hipStream_t s, bool f16) {
     if (g_conv3_mode == 0) return false;
+    // the staggered two-wave-group kernel (c_out = 128, or c_in = c_out = 64)
+    if (g_conv3_mode == 1 && launch_conv3s(a, s, f16)) return true;
     if (a.kh != 3 || a.kw != 3 || a.stride != 1 || a.pad != 1 || a.dil != 1) return false;
     if (!(a.flags & RR_CONV_PERM32) || (a.flags & RR_CONV_RESIDUAL) || a.ldy != a.cout) return false;
     if (a.cin % 64 || a.kp != 9 * a.cin || a.w_ % 32) return false;

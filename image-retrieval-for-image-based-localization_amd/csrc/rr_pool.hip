@@ -353,6 +353,8 @@ int rr_global_pool_pdev(const void* x, int n, int c, int hw, int layout, int mod
                         float eps, float* out, int dtype, void* stream) {
     if (n <= 0 || c <= 0 || hw <= 0) return fail(RR_EINVAL, "rr_global_pool: empty input");
     if (mode < 0 || mode > 2) return fail(RR_EINVAL, "rr_global_pool: mode");
+    // the host exponent is validated here; a device exponent (p_dev) is read by the kernel
+    if (mode == RR_POOL_GEM && !p_dev && !(p > 0.f)) return fail(RR_EINVAL, "rr_global_pool: GeM p must be > 0");
     const float* pdev = mode == RR_POOL_GEM ? p_dev : nullptr;
     int ip = (p == 3.f) ? 3 : (p == 2.f) ? 2 : (p == 1.f) ? 1 : 0;
     hipStream_t s = as_stream(stream);

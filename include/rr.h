@@ -289,12 +289,15 @@ int rr_mutual_nn(const long long* nn12, int n1, const long long* nn21, int n2, l
  *                        conv before BN/activation, exact by monotonicity); 0: v1 (BN/activation
  *                        on every stem pixel).  Odd stem maps always take v1.
  *   RR_TUNE_STREAM_XCD   1 (default): the streaming 1x1's channel-slice blocks of one pixel
- *                        strip run on one XCD (the strip's input is re-read from that L2) */
+ *                        strip run on one XCD (the strip's input is re-read from that L2)
+ *   RR_TUNE_CONV3S       1 (default): the staggered two-wave-group direct 3x3 (persistent,
+ *                        chunk-double-buffered halo patches) for the stride-1 3x3s with
+ *                        c_out = 128 or c_in = c_out = 64 under RR_TUNE_CONV3X3 = 1; 0 off */
 enum rr_tune_key { RR_TUNE_GEMM_CONFIG = 0, RR_TUNE_GEMM_STAGES = 1, RR_TUNE_GEMM_WIDE = 2,
                    RR_TUNE_GEMM_ASTAT = 3, RR_TUNE_GEMM_XCD_MAP = 4, RR_TUNE_STREAM_1X1 = 5,
                    RR_TUNE_CONV3X3 = 6, RR_TUNE_GRID_CUS = 7, RR_TUNE_GEMM8 = 8,
                    RR_TUNE_KNN_FUSED = 9, RR_TUNE_CONV3_PIPE = 10,
-                   RR_TUNE_STEM = 11, RR_TUNE_STREAM_XCD = 12 };
+                   RR_TUNE_STEM = 11, RR_TUNE_STREAM_XCD = 12, RR_TUNE_CONV3S = 13 };
 int rr_set_tuning(int key, int value);
 
 /* ----------------------------------------------------------- data helpers */

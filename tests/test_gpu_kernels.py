@@ -170,6 +170,40 @@ def test_conv3x3_pipelined_schedule_bit_identical(cuda, prec):
     assert torch.equal(outs[0], outs[1])
 
 
+CONV3S_CASES = [
+    # (case, grid cap): the staggered persistent direct 3x3 (rr_conv3s.hip); a CU cap
+    # gives small problems several tiles per block and ragged XCD ranges
+    ((3, 64, 48, 96, 64, 3, 1, 1, False, True), 8),      # mod2 form: 27 tiles of 16 x 32 over 8 blocks
+    ((2, 64, 32, 64, 64, 3, 1, 1, False, False), 8),     # identity activation, 2 tiles per block
+    ((3, 128, 24, 96, 128, 3, 1, 1, False, True), 8),    # mod3 form: 2 chunks, 27 tiles of 8 x 32
+    ((3, 64, 24, 96, 128, 3, 1, 1, False, True), 8),     # one chunk: patch buffers alternate per tile
+    ((4, 256, 16, 64, 128, 3, 1, 1, False, True), 8),    # 4 chunks
+    ((5, 128, 16, 32, 128, 3, 1, 1, False, True), 16),   # 10 tiles < 2 per block: falls back to k_conv3x3
+    ((8, 64, 192, 256, 64, 3, 1, 1, False, True), 0),    # mod2 at 768x1024, whole chip
+    ((16, 128, 96, 128, 128, 3, 1, 1, False, True), 0),  # mod3 at 768x1024, whole chip
+]
+
+
+@pytest.mark.parametrize("case,cap", CONV3S_CASES)
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_conv3s_staggered(cuda, case, cap, prec):
+    """Staggered two-wave-group direct 3x3 (RR_TUNE_CONV3S) vs float64; the
+    c_out = 128 form accumulates in k_conv3x3's (chunk, tap, half-step) order,
+    so it is also bit-identical to it."""
+    from cirtorch import _engine as E
+    outs = []
+    try:
+        E.check(E.lib().rr_set_tuning(7, cap), "rr_set_tuning")
+        for on in (1, 0):
+            E.check(E.lib().rr_set_tuning(13, on), "rr_set_tuning")
+            outs.append(_check_conv(cuda, case, prec, True))
+    finally:
+        E.lib().rr_set_tuning(13, 1)
+        E.lib().rr_set_tuning(7, 0)
+    if case[4] == 128:
+        assert torch.equal(outs[0], outs[1])
+
+
 def _check_conv(cuda, case, prec, perm):
     n, cin, h, w, cout, k, s, p, use_res, leaky = case
     g = torch.Generator().manual_seed(hash(case) & 0xFFFF)

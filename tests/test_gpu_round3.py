@@ -1,0 +1,152 @@
+"""GPU checks of the round-3 surface through librr.so: a ResidualBlock called on
+its own (reference ``cirtorch/backbones/misc.py:184-203``), a model built the
+``make_model`` way (``scripts/train_globalF.py:240-356``) extracting the same
+descriptors after a snapshot round trip (``utils/snapshot.py:41-75``), and the
+multi-scale forward's loss dict (``models/GF_net.py:89-92``)."""
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from test_host_round3 import _body_section, _make_model
+
+pytestmark = pytest.mark.gpu
+
+
+def _block_reference(blk, x):
+    """float64 restatement of ResidualBlock.forward (misc.py:163-203) with eval BN"""
+    def bn(m, t):
+        inv = torch.rsqrt(m.running_var.double() + m.eps)
+        s = m.weight.double() * inv
+        return t * s[None, :, None, None] + (m.bias.double() - m.running_mean.double() * s)[None, :, None, None]
+
+    def act(m, t):
+        return F.leaky_relu(t, m.activation_param) if m.activation == "leaky_relu" else t
+
+    c = blk.convs
+    names = ["1", "2", "3"] if blk.is_bottleneck else ["1", "2"]
+    y = x
+    for i, k in enumerate(names):
+        conv, b = getattr(c, "conv" + k), getattr(c, "bn" + k)
+        y = bn(b, F.conv2d(y, conv.weight.double(), stride=conv.stride, padding=conv.padding))
+        if i + 1 < len(names):
+            y = act(b, y)
+    res = bn(blk.proj_bn, F.conv2d(x, blk.proj_conv.weight.double(), stride=blk.proj_conv.stride)) \
+        if hasattr(blk, "proj_conv") else x
+    return act(c.bn1, y + res)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16", "fp16"])
+@pytest.mark.parametrize("arch,mod,block", [("resnet50", 3, 1), ("resnet50", 2, 2), ("resnet18", 4, 1)])
+def test_residual_block_standalone(cuda, precision, arch, mod, block):
+    from cirtorch.backbones import resnet
+    from cirtorch.models.init import random_init_
+    body = resnet.__dict__[arch](precision=precision)
+    random_init_(body, 3)
+    blk = getattr(getattr(body, "mod%d" % mod), "block%d" % block)
+    cin = blk.convs.conv1.in_channels
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(2, cin, 24, 32, generator=g)
+    body = body.to(cuda).eval()
+    dt = body.engine_dtype
+    xq = x.to(dt).float()  # the engine's operand rounding of the input
+    ref = _block_reference(blk.cpu(), xq.double())
+    blk.to(cuda)
+    got = blk(x.to(cuda))
+    assert got.dtype == torch.float32 and got.shape == ref.shape
+    err = (got.cpu().double() - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    tol = {"fp32": 2e-5, "bf16": 3e-2, "fp16": 5e-3}[precision]
+    assert err <= tol * scale, (err, scale)
+    # in the engine dtype the block returns an NCHW-shaped view of its NHWC buffer
+    got16 = blk(x.to(cuda).to(dt))
+    assert got16.dtype == dt and got16.shape == ref.shape
+
+
+def test_block_chain_equals_body_stage(cuda):
+    """fp32: the stage map of the fused body equals its blocks called one by one"""
+    from cirtorch.backbones import resnet
+    from cirtorch.models.init import random_init_
+    body = resnet.resnet50(precision="fp32")
+    random_init_(body, 5)
+    body = body.to(cuda).eval()
+    x = torch.rand(2, 3, 128, 160, device=cuda)
+    with torch.no_grad():
+        outs = body(x)
+        t = outs["mod3"].float()
+        for blk in body.mod4.children():
+            t = blk(t)
+    assert torch.equal(t, outs["mod4"].float())
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_make_model_snapshot_descriptors(cuda, tmp_path, precision):
+    """the make_model-built net extracts the same descriptors after
+    save_snapshot -> resume_from_snapshot into a fresh net (engine plans rebuilt)"""
+    from cirtorch.models.init import random_init_
+    from cirtorch.utils.snapshot import resume_from_snapshot, save_snapshot
+    cp = _body_section()
+    src, _, _ = _make_model(cp, "resnet50")
+    random_init_(src, 7)
+    src.body.set_precision(precision)
+    path = str(tmp_path / "snap.pth")
+    save_snapshot(path, cp, 1, 0.0, 0.0, 10, body=src.body.state_dict(), ret_head=src.ret_head.state_dict())
+    src = src.to(cuda).eval()
+    imgs = torch.rand(2, 3, 224, 288, device=cuda)
+    ref = src.extract(imgs)
+    dst, _, _ = _make_model(cp, "resnet50")
+    random_init_(dst, 8)
+    dst.body.set_precision(precision)
+    dst = dst.to(cuda).eval()
+    before = dst.extract(imgs)
+    resume_from_snapshot(dst, path, ["body", "ret_head"])
+    dst = dst.to(cuda)
+    got = dst.extract(imgs)
+    assert not torch.equal(before, ref)
+    assert torch.equal(got, ref)
+
+
+def test_multiscale_forward_returns_loss_dict(cuda):
+    from cirtorch.models.GF_net import make_net
+    from cirtorch.models.init import random_init_
+    net = random_init_(make_net("resnet18", precision="bf16"), 1).to(cuda).eval()
+    imgs = torch.rand(2, 3, 96, 128, device=cuda)
+    with torch.no_grad():
+        for img in (imgs, list(imgs)):
+            loss, pred = net(img=img, scales=[0.5, 1])
+            assert list(loss.keys()) == ["ret_loss"] and loss["ret_loss"] is None
+            assert pred["ret_pred"].shape == (512, 2)
+
+
+def test_fp16_overflow_falls_back_to_bf16(cuda):
+    """a checkpoint whose activations leave fp16 range (stem BN gamma x 1e6): the fp16
+    descriptors would be inf / NaN; extract_vectors returns the bf16 ones instead"""
+    from cirtorch.models.GF_net import extract_vectors, make_net
+    from cirtorch.models.init import random_init_
+    net = random_init_(make_net("resnet18", precision="fp16", mean=[0.485, 0.456, 0.406],
+                                std=[0.229, 0.224, 0.225]), 2)
+    with torch.no_grad():
+        net.body.mod1.bn1.weight.mul_(1e6)
+    net.body.refresh_engine()
+    net = net.to(cuda).eval()
+    imgs = [torch.randint(0, 256, (3, 96, 128), dtype=torch.uint8) for _ in range(3)]
+    with torch.no_grad():
+        raw = net.extract(torch.stack(imgs).to(cuda))
+    assert not torch.isfinite(raw).all()  # the fp16 chain overflowed
+    with pytest.warns(UserWarning, match="overflowed fp16"):
+        got = extract_vectors(net, imgs, None, batch=2)
+    assert net.body.engine_dtype == torch.float16
+    net.body.set_precision("bf16")
+    ref = extract_vectors(net, imgs, None, batch=2)
+    assert torch.isfinite(got).all() and torch.equal(got, ref)
+
+
+def test_extract_vectors_device_tensors(cuda):
+    """same-size GPU tensors are stacked on the device (no pinned host staging)"""
+    from cirtorch.models.GF_net import extract_vectors, make_net
+    from cirtorch.models.init import random_init_
+    net = random_init_(make_net("resnet18", precision="bf16"), 4).to(cuda).eval()
+    imgs = [torch.rand(3, 64, 96) for _ in range(3)]
+    host = extract_vectors(net, imgs, None, batch=4)
+    dev = extract_vectors(net, [t.to(cuda) for t in imgs], None, batch=4)
+    assert torch.equal(host, dev)
