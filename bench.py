@@ -79,6 +79,8 @@ def parse():
     ap.add_argument("--extract-priority", type=int, default=int(os.environ.get("RR_BENCH_PRIO", "0")),
                     help="1: run the extraction on a high-priority stream (the overlapped search keeps the default)")
     ap.add_argument("--tune", default="", help="developer A/B: rr_set_tuning pairs key=value[,key=value]")
+    ap.add_argument("--fp16-steps", type=int, default=10,
+                    help="steps of the fp16 end-to-end line (e2e_fp16; 0 = skip)")
     return ap.parse_args()
 
 
@@ -191,6 +193,41 @@ def host_cpu():
         pass
     return model, max(1, len(phys))
 
+
+
+def kernel_source_digest():
+    """sha1 (12 hex) of the HIP sources of librr.so (csrc/*.hip, *.h, include/rr.h): a PMC
+    traffic file is attached to the roofline only if it was collected on these sources."""
+    import glob
+    import hashlib
+    h = hashlib.sha1()
+    files = sorted(glob.glob(os.path.join(PKG, "csrc", "*.hip")) + glob.glob(os.path.join(PKG, "csrc", "*.h"))) + \
+        [os.path.join(REPO, "include", "rr.h")]
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:12]
+
+
+def pmc_file(kind, match):
+    """newest profiles/r*_pmc_<kind>.json whose config satisfies match(config) ->
+    (data, path, fresh): fresh = collected on the current kernel sources"""
+    import glob
+    digest = kernel_source_digest()
+    best = None
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_%s.json" % kind)), reverse=True):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        c = d.get("config", {})
+        if not match(c):
+            continue
+        fresh = c.get("source_digest") == digest
+        if fresh:
+            return d, path, True
+        best = best or (d, path, False)
+    return best if best else (None, None, False)
 
 
 GOLDEN = os.path.join(REPO, "tests", "golden")
@@ -512,11 +549,13 @@ def main():
     main_stream = torch.cuda.current_stream(dev)
     match_stream = torch.cuda.Stream(dev) if args.overlap else main_stream
 
+    state = {"net": net, "index": index}
+
     def match(desc):
         q = desc.t().contiguous()
         if world > 1:
             q = all_gather_stacked(q).reshape(world * B, q.shape[1])
-        return index.search(q, args.k)
+        return state["index"].search(q, args.k)
 
     EB = max(1, min(args.extract_batch, B))
 
@@ -527,7 +566,7 @@ def main():
             if record:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(main_stream)
-            descs.append(net.extract(images[c:c + EB]))
+            descs.append(state["net"].extract(images[c:c + EB]))
             if record:
                 e1.record(main_stream)
                 ev_pairs.append((e0, e1))
@@ -561,6 +600,37 @@ def main():
             dist.barrier()
         elapsed = max_over_ranks(time.perf_counter() - t0)
         body_ms = sum(a.elapsed_time(b) for a, b in ev_pairs) / args.steps   # extractor time per step
+
+        # the same step with fp16 operands / activations and an fp16-screened
+        # index: the precision that meets the north_star descriptor bar
+        e2e_fp16 = None
+        if args.fp16_steps > 0 and args.precision == "bf16":
+            net16 = make_net(args.arch, precision="fp16", mean=[0.485, 0.456, 0.406], std=[0.229, 0.224, 0.225])
+            random_init_(net16, seed=0)
+            net16 = net16.to(dev).eval()
+            index16 = ShardedIndex(db32, r0, precision="fp16")
+            saved = (state["net"], state["index"])
+            state["net"], state["index"] = net16, index16
+            for _ in range(2):
+                step(False)
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            t16 = time.perf_counter()
+            for _ in range(args.fp16_steps):
+                step(False)
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            el16 = max_over_ranks(time.perf_counter() - t16)
+            state["net"], state["index"] = saved
+            e2e_fp16 = {"value": world * B * args.fp16_steps / el16, "unit": "images/s",
+                        "ms_per_step": el16 / args.fp16_steps * 1e3, "steps": args.fp16_steps,
+                        "note": "the headline step (extract B images + top-k search of all queries vs the sharded "
+                                "1M DB) with fp16 operands/activations and an fp16 screening copy; descriptor "
+                                "cosine vs the reference: precisions.fp16"}
+            del net16, index16
+            torch.cuda.empty_cache()
 
         # extract-only loop (same net, no matching)
         torch.cuda.synchronize()
@@ -646,27 +716,32 @@ def main():
                    "roofline": {"bound": "mfma", "achieved": flops / tk / 1e12, "peak": peak, "unit": "TFLOP/s",
                                 "frac": flops / tk / 1e12 / peak, "traffic": None,
                                 "note": "per-rank screening GEMM FLOPs 2*Q*n_local*D / whole search time"}}
-            kpath = os.path.join(REPO, "profiles", "r02_pmc_knn_q%d.json" % args.knn_q)
-            if os.path.exists(kpath) and world == 1:
-                kt = json.load(open(kpath))
+            kt, kpath, kfresh = pmc_file("knn_q%d" % args.knn_q, lambda c: (
+                c.get("db_rows"), c.get("dim"), c.get("k"), c.get("screen")) == (
+                args.db_rows, args.dim, args.k, args.precision))
+            if kt is not None and world == 1:
                 kc = kt.get("config", {})
-                if (kc.get("db_rows"), kc.get("dim"), kc.get("k"), kc.get("screen")) == (
-                        args.db_rows, args.dim, args.k, args.precision):
+                if kfresh:
                     knn["roofline"]["traffic"] = kt["hbm_bytes_per_search"]
-                    knn["roofline"]["traffic_note"] = (
-                        "HBM bytes of one search from rocprofv3 PMC (2 x FETCH_SIZE + WRITE_SIZE), %s, commit %s"
-                        % (os.path.relpath(kpath, REPO), kc.get("source_commit", "?")))
+                knn["roofline"]["traffic_note"] = (
+                    "HBM bytes of one search from rocprofv3 PMC (2 x FETCH_SIZE + WRITE_SIZE), %s, commit %s%s"
+                    % (os.path.relpath(kpath, REPO), kc.get("source_commit", "?"),
+                       "" if kfresh else "; STALE (kernel sources changed since: digest %s vs %s), not attached"
+                       % (kc.get("source_digest", "?"), kernel_source_digest())))
 
     traffic, traffic_note = None, "no PMC traffic file for this config"
-    tpath = os.path.join(REPO, "profiles", "r02_pmc_traffic.json")
-    if os.path.exists(tpath):
-        t = json.load(open(tpath))
+    t, tpath, tfresh = pmc_file("traffic", lambda c: (c.get("arch"), c.get("precision"), c.get("image")) == (
+        args.arch, args.precision, [3, H, W]))
+    if t is not None:
         c = t.get("config", {})
-        if (c.get("arch"), c.get("precision"), c.get("image")) == (args.arch, args.precision, [3, H, W]):
+        if tfresh:
             traffic = t["hbm_bytes_per_image"] * B
-            traffic_note = ("HBM bytes of the step's extractor dispatches from rocprofv3 PMC (2 x FETCH_SIZE + "
-                            "WRITE_SIZE, profiles/r02_pmc_traffic.json, %d-image forwards, commit %s)"
-                            % (c.get("batch", 0), c.get("source_commit", "?")))
+        traffic_note = ("HBM bytes of the step's extractor dispatches from rocprofv3 PMC (2 x FETCH_SIZE + "
+                        "WRITE_SIZE, %s, %d-image forwards, commit %s, kernel-source digest %s)%s"
+                        % (os.path.relpath(tpath, REPO), c.get("batch", 0), c.get("source_commit", "?"),
+                           c.get("source_digest", "?"), "" if tfresh else
+                           "; STALE: the kernel sources changed since (current digest %s), not attached"
+                           % kernel_source_digest()))
     # local-descriptor head: 2048 keypoints per image on an
     # R50 mod4-shaped bf16 map (1024 ch at H/16 x W/16), E = 128, + mutual NN of two images
     local = None
@@ -766,6 +841,10 @@ def main():
                             "note": "sum over the body's 53 conv layers of max(FLOPs/peak_mfma, algorithmic HBM bytes/"
                                     "peak_hbm) for the step's images, over the measured extractor time"},
         "extract_images_per_sec": ext_only * world,
+        "dist": {"world_size": dist.get_world_size() if dist.is_initialized() else 1,
+                 "backend": dist.get_backend() if dist.is_initialized() else None,
+                 "note": "backend nccl = RCCL over xGMI on ROCm"},
+        "e2e_fp16": e2e_fp16,
         "knn": knn,
         "local": local,
         "latency": latency,

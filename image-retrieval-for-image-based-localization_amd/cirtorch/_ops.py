@@ -46,15 +46,21 @@ def pack_conv_weights(weight, cin_pad, dtype, perm32=False, k_mult=64):
 
 
 def conv2d_fused(x, w_packed, kh, kw, stride, pad, c_out, scale=None, shift=None, residual=None,
-                 leaky=True, slope=0.01, out_dtype=None, dil=1, perm32=False):
+                 leaky=True, slope=0.01, out_dtype=None, dil=1, perm32=False, out=None):
     """x: [N, H, W, C] -> act(conv(x) * scale + shift (+ residual)) as [N, Ho, Wo, c_out].
-    perm32: w_packed rows are in the RR_CONV_PERM32 order (pack_conv_weights(perm32=True))."""
+    perm32: w_packed rows are in the RR_CONV_PERM32 order (pack_conv_weights(perm32=True)).
+    out: an optional contiguous [N, Ho, Wo, c_out] destination (e.g. a batch slice)."""
     E.require_gpu(x, w_packed)
     n, h, w, c = x.shape
     ho = (h + 2 * pad - dil * (kh - 1) - 1) // stride + 1
     wo = (w + 2 * pad - dil * (kw - 1) - 1) // stride + 1
     out_dtype = out_dtype or x.dtype
-    y = torch.empty((n, ho, wo, c_out), dtype=out_dtype, device=x.device)
+    if out is not None:
+        E.require_gpu(out)
+        assert tuple(out.shape) == (n, ho, wo, c_out) and out.dtype == out_dtype and out.is_contiguous()
+        y = out
+    else:
+        y = torch.empty((n, ho, wo, c_out), dtype=out_dtype, device=x.device)
     flags = 0
     if scale is not None:
         flags |= E.RR_CONV_AFFINE

@@ -43,10 +43,10 @@ def make_step(conv, bn, dtype, cin_pad=None, leaky_override=None):
     return st
 
 
-def run_step(t, st, residual=None):
-    """NHWC t -> NHWC conv + BN (+ residual) + activation"""
+def run_step(t, st, residual=None, out=None):
+    """NHWC t -> NHWC conv + BN (+ residual) + activation (into `out` when given)"""
     return _ops.conv2d_fused(t, st.w, st.kh, st.kw, st.stride, st.pad, st.c_out, st.scale, st.shift,
-                             residual=residual, leaky=st.leaky, slope=st.slope, perm32=st.perm)
+                             residual=residual, leaky=st.leaky, slope=st.slope, perm32=st.perm, out=out)
 
 
 class ResidualBlock(nn.Module):

@@ -177,31 +177,26 @@ class ResNet(nn.Module):
         return plan
 
     @staticmethod
-    def _conv(t, st, residual=None):
-        return run_step(t, st, residual)
+    def _conv(t, st, residual=None, out=None):
+        return run_step(t, st, residual, out)
 
-    def forward(self, x, normalize=None):
-        """x: [N, 3, H, W] float32 on the GPU, or uint8 pixels (read as x / 255) (already normalised unless
-        ``normalize=(mean, std)`` is given, which fuses cirtorch/utils/image.py
-        ``normalize`` into the first kernel).  Returns OrderedDict mod1..mod5."""
-        plan = self._plan or self._build_plan()
-        mean, std = normalize if normalize is not None else (None, None)
+    def _stem(self, plan, x, mean, std):
         if x.dtype == torch.uint8 and plan["stem_fused"] is None:
             x = _ops.pixels_to_unit(x)  # pixels -> [0, 1] (to_tensor); the fused stem reads uint8 itself
         if plan["stem_fused"] is not None:
             st = plan["stem"]
-            t = _ops.stem_conv_pool(x, plan["stem_fused"], st.scale, st.shift, leaky=st.leaky, slope=st.slope,
-                                    mean=mean, std=std)
-        else:
-            t = _ops.image_to_nhwc(x, self.stem_cin(), self.engine_dtype, mean, std)
-            t = self._conv(t, plan["stem"])
-            t = _ops.maxpool2d(t, 3, 2, 1)
-        outs = OrderedDict()
-        outs["mod1"] = t
-        flat = [(mod_id, steps, proj) for mod_id, blocks in enumerate(plan["mods"]) for steps, proj in blocks]
-        pending = None  # conv1 output of the next block, produced by a fused boundary launch
-        for i, (mod_id, steps, proj) in enumerate(flat):
-            nxt = flat[i + 1][1][0] if i + 1 < len(flat) else None
+            return _ops.stem_conv_pool(x, plan["stem_fused"], st.scale, st.shift, leaky=st.leaky, slope=st.slope,
+                                       mean=mean, std=std)
+        t = _ops.image_to_nhwc(x, self.stem_cin(), self.engine_dtype, mean, std)
+        t = self._conv(t, plan["stem"])
+        return _ops.maxpool2d(t, 3, 2, 1)
+
+    def _blocks(self, t, flat, i0, i1, outs, pending=None):
+        """blocks flat[i0:i1] on the NHWC map t (the conv1 output of block i0 may come
+        precomputed as `pending`); stage maps into outs (when not None)."""
+        for i in range(i0, i1):
+            mod_id, steps, proj = flat[i]
+            nxt = flat[i + 1][1][0] if i + 1 < i1 else None
             pair = self._pairable(steps[-1], nxt)
             fuse_proj = pair and proj is not None and self._proj_fusable(proj)
             res = t if proj is None else (None if fuse_proj else self._conv(t, proj))
@@ -216,8 +211,21 @@ class ResNet(nn.Module):
                                                proj=(t, proj.w, proj.scale, proj.shift) if fuse_proj else None)
             else:
                 t = self._conv(y, steps[-1], residual=res)
-            if i + 1 == len(flat) or flat[i + 1][0] != mod_id:
+            if outs is not None and (i + 1 == len(flat) or flat[i + 1][0] != mod_id):
                 outs["mod%d" % (mod_id + 2)] = t
+        return t, pending
+
+    def forward(self, x, normalize=None):
+        """x: [N, 3, H, W] float32 on the GPU, or uint8 pixels (read as x / 255) (already normalised unless
+        ``normalize=(mean, std)`` is given, which fuses cirtorch/utils/image.py
+        ``normalize`` into the first kernel).  Returns OrderedDict mod1..mod5."""
+        plan = self._plan or self._build_plan()
+        mean, std = normalize if normalize is not None else (None, None)
+        outs = OrderedDict()
+        flat = [(mod_id, steps, proj) for mod_id, blocks in enumerate(plan["mods"]) for steps, proj in blocks]
+        t = self._stem(plan, x, mean, std)
+        outs["mod1"] = t
+        self._blocks(t, flat, 0, len(flat), outs)
         return OrderedDict((k, v.permute(0, 3, 1, 2)) for k, v in outs.items())
 
     @staticmethod

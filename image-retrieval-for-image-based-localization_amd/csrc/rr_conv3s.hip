@@ -17,7 +17,8 @@
 //   * operands arrive by LDS-DMA (buffer_load ... lds) tracked by counted
 //     vmcnt, each LDS region overwritten no earlier than two phases after its
 //     last read (the rule that keeps the lagging group's reads safe).
-// Two variants:
+// Two variants (mod3 / mod2 of R50; measured 442-454 vs 532 us and 533-554 vs
+// 525 us at 128 images, so only the first is on by default):
 //   k_c3s_w128  c_out = 128, c_in = 64 * nck (mod3: 128): 8 x 32 output tile;
 //               per 64-channel input chunk a (8+2) x (32+2) halo patch
 //               (128 B per pixel) double-buffered by chunk — the next chunk
@@ -513,7 +514,9 @@ __global__ void __launch_bounds__(512, 1) k_c3s_w64(ConvArgs a, int tiles_w, int
 
 }  // namespace
 
-int g_conv3s = 1;  // rr_set_tuning(RR_TUNE_CONV3S): 1 staggered direct 3x3 where eligible (default), 0 off
+int g_conv3s = 1;  // rr_set_tuning(RR_TUNE_CONV3S): 0 off, 1 auto (default): the c_out = 128 form;
+                   // 2 also the c_in = c_out = 64 form (measured 533-554 vs 525 us for k_conv3x3
+                   // at 128 x R50 mod2: HBM-latency bound there, see DESIGN)
 
 // bf16 / fp16 3x3 / stride 1 / pad 1, PERM32 weights, no residual, one
 // channel tile (c_out = 128 with c_in % 64 == 0, or c_in = c_out = 64), image
@@ -525,7 +528,7 @@ bool launch_conv3s(const ConvArgs& a, hipStream_t s, bool f16) {
     if (a.act == RR_ACT_LEAKY && !(a.slope >= 0.f && a.slope <= 1.f)) return false;
     if (a.kp != 9 * a.cin || a.w_ % 32) return false;
     if ((long long)a.n * a.h * a.w_ * a.cin * 2 >= (1ll << 31) || (long long)a.cout * a.kp * 2 >= (1ll << 31)) return false;
-    const bool w64 = a.cin == 64 && a.cout == 64 && a.h % 16 == 0;
+    const bool w64 = g_conv3s == 2 && a.cin == 64 && a.cout == 64 && a.h % 16 == 0;
     const bool w128 = a.cout == 128 && a.cin % 64 == 0 && a.h % 8 == 0;
     if (!w64 && !w128) return false;
     const int th = w64 ? 16 : 8;

@@ -292,7 +292,7 @@ int rr_mutual_nn(const long long* nn12, int n1, const long long* nn21, int n2, l
  *                        strip run on one XCD (the strip's input is re-read from that L2)
  *   RR_TUNE_CONV3S       1 (default): the staggered two-wave-group direct 3x3 (persistent,
  *                        chunk-double-buffered halo patches) for the stride-1 3x3s with
- *                        c_out = 128 or c_in = c_out = 64 under RR_TUNE_CONV3X3 = 1; 0 off */
+ *                        c_out = 128 under RR_TUNE_CONV3X3 = 1; 2: also c_in = c_out = 64; 0 off */
 enum rr_tune_key { RR_TUNE_GEMM_CONFIG = 0, RR_TUNE_GEMM_STAGES = 1, RR_TUNE_GEMM_WIDE = 2,
                    RR_TUNE_GEMM_ASTAT = 3, RR_TUNE_GEMM_XCD_MAP = 4, RR_TUNE_STREAM_1X1 = 5,
                    RR_TUNE_CONV3X3 = 6, RR_TUNE_GRID_CUS = 7, RR_TUNE_GEMM8 = 8,

@@ -194,14 +194,16 @@ def test_conv3s_staggered(cuda, case, cap, prec):
     outs = []
     try:
         E.check(E.lib().rr_set_tuning(7, cap), "rr_set_tuning")
-        for on in (1, 0):
+        # 2: both forms (the c_in = c_out = 64 one is opt-in), 1: default, 0: k_conv3x3
+        for on in (2, 1, 0):
             E.check(E.lib().rr_set_tuning(13, on), "rr_set_tuning")
             outs.append(_check_conv(cuda, case, prec, True))
     finally:
         E.lib().rr_set_tuning(13, 1)
         E.lib().rr_set_tuning(7, 0)
+    # the c_out = 128 form accumulates in k_conv3x3's (chunk, tap, half-step) order
     if case[4] == 128:
-        assert torch.equal(outs[0], outs[1])
+        assert torch.equal(outs[0], outs[2]) and torch.equal(outs[1], outs[2])
 
 
 def _check_conv(cuda, case, prec, perm):

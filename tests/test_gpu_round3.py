@@ -150,3 +150,4 @@ def test_extract_vectors_device_tensors(cuda):
     host = extract_vectors(net, imgs, None, batch=4)
     dev = extract_vectors(net, [t.to(cuda) for t in imgs], None, batch=4)
     assert torch.equal(host, dev)
+

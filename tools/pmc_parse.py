@@ -9,6 +9,7 @@ coalesced read: x2; WRITE_SIZE exact for 16-B stores; both in KiB).
 
 import argparse
 import csv
+import sys
 import glob
 import json
 import os
@@ -40,6 +41,7 @@ def main():
     ap.add_argument("write_dir")
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--config", default="{}", help="JSON config of the workload (bench.py matches on it)")
     args = ap.parse_args()
     f_kib, nf, fk = load(args.fetch_dir, "FETCH_SIZE")
     w_kib, nw, wk = load(args.write_dir, "WRITE_SIZE")
@@ -54,6 +56,16 @@ def main():
                      "wide reads), write = WRITE_SIZE; KiB -> bytes",
            "per_kernel_read_bytes": {k: 2.0 * v[0] * 1024 / args.iters for k, v in fk.items()},
            "per_kernel_write_bytes": {k: v[0] * 1024 / args.iters for k, v in wk.items()}}
+    # the kernel sources the counters were collected on (bench.py attaches the
+    # traffic to its roofline only while the digest still matches)
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import kernel_source_digest
+    cfg = json.loads(args.config)
+    cfg["source_digest"] = kernel_source_digest()
+    cfg["source_commit"] = os.environ.get("RR_SOURCE_COMMIT", "?")
+    out["config"] = cfg
+    if "screen" in cfg:  # a kNN search workload
+        out["hbm_bytes_per_search"] = out["hbm_bytes_per_forward"]
     print(json.dumps(out, indent=1))
 
 

@@ -19,9 +19,11 @@ for C in FETCH_SIZE WRITE_SIZE; do
 done
 timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$OUT/body_mfma" -o run \
   --output-format csv -- python3 "$ROOT/tools/pmc_body.py" --batch 128 > "$OUT/body_mfma.log" 2>&1
-python3 "$ROOT/tools/pmc_parse.py" "$OUT/body_FETCH_SIZE" "$OUT/body_WRITE_SIZE" --iters 3 --batch 128 > "$OUT/traffic_body.json"
+python3 "$ROOT/tools/pmc_parse.py" "$OUT/body_FETCH_SIZE" "$OUT/body_WRITE_SIZE" --iters 3 --batch 128 \
+  --config '{"arch": "resnet50", "precision": "bf16", "image": [3, 768, 1024], "batch": 128}' > "$OUT/traffic_body.json"
 for Q in 128 1024; do
   python3 "$ROOT/tools/pmc_parse.py" "$OUT/knn${Q}_FETCH_SIZE" "$OUT/knn${Q}_WRITE_SIZE" --iters 3 --batch $Q \
+    --config "{\"db_rows\": 1000000, \"dim\": 2048, \"k\": 100, \"screen\": \"bf16\", \"q\": $Q}" \
     > "$OUT/traffic_knn$Q.json"
 done
 python3 "$ROOT/tools/pmc_mfma.py" "$OUT/body_mfma" --iters 3 > "$OUT/mfma_body.json"
