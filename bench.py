@@ -452,49 +452,72 @@ def bench_config4(args, images, dev):
                     "f64-MFMA whitenapply), full GPU ranks 4993 x 70, vectorised E/M/H mAP"}
 
 
+def decode_workers():
+    """host decode threads: the CPUs this process may run on, capped at 16 (the GPU box's
+    CPU share per GPU; nproc there reports the whole machine)"""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
 def bench_dropin(net, H, W, dev, n_files=128, distinct=16):
     """The drop-in path scripts/test.py calls (extract_vectors, :236-238) on
-    n_files same-size PNG files (compress_level 1): PIL decode on 16 host
-    threads + batched uint8 chains, vs the same images already decoded."""
+    n_files same-size image files: PNG (compress_level 1) and JPEG (quality 90,
+    the reference datasets' format, cirtorch/datasets/globalFeatures/misc.py:17-30);
+    PIL decode on the host's decode threads + batched uint8 chains, vs the same
+    images already decoded."""
     import shutil
     import tempfile
     import numpy as np
     from PIL import Image
     from cirtorch.models.GF_net import extract_vectors, _decode
+    workers = decode_workers()
     d = tempfile.mkdtemp(prefix="rr_dropin_")
     try:
         r = np.random.default_rng(3)
-        paths = []
+        paths = {"png": [], "jpg": []}
         for i in range(distinct):
             field = r.random((6, 8, 3))
             up = np.kron(field, np.ones((H // 6 + 1, W // 8 + 1, 1)))[:H, :W]
             arr = (np.clip(0.8 * up + 0.2 * r.random((H, W, 3)), 0, 1) * 255).astype(np.uint8)
             p = os.path.join(d, "im%02d.png" % i)
             Image.fromarray(arr).save(p, compress_level=1)
-            paths.append(p)
-        paths = [paths[i % distinct] for i in range(n_files)]
-        extract_vectors(net, paths[:8], None, workers=16)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        extract_vectors(net, paths, None, workers=16)
-        t_files = time.perf_counter() - t0
-        dec = [_decode(p, None, None, None, None) for p in paths]
+            paths["png"].append(p)
+            p = os.path.join(d, "im%02d.jpg" % i)
+            Image.fromarray(arr).save(p, quality=90)
+            paths["jpg"].append(p)
+        out = {}
+        for fmt in ("png", "jpg"):
+            ps = [paths[fmt][i % distinct] for i in range(n_files)]
+            extract_vectors(net, ps[:8], None, workers=workers)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            v = extract_vectors(net, ps, None, workers=workers)
+            out["%s_files_images_per_sec" % fmt] = n_files / (time.perf_counter() - t0)
+            t0 = time.perf_counter()
+            for p in ps[:32]:
+                _decode(p, None, None, None, None)
+            out["%s_decode_ms_per_image_one_thread" % fmt] = (time.perf_counter() - t0) / 32 * 1e3
+            if fmt == "jpg":
+                one = extract_vectors(net, ps[:1], None, workers=1)   # batch-1 result of the same file
+                out["jpg_equals_batch1"] = bool(torch.equal(v[:, :1], one))
+                dec = [_decode(p, None, None, None, None) for p in ps]
         extract_vectors(net, dec[:8], None)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         extract_vectors(net, dec, None)
         t_dec = time.perf_counter() - t0
-        t0 = time.perf_counter()
-        for p in paths[:32]:
-            _decode(p, None, None, None, None)
-        t_one = (time.perf_counter() - t0) / 32
     finally:
         shutil.rmtree(d, ignore_errors=True)
-    return {"png_files_images_per_sec": n_files / t_files, "decoded_uint8_images_per_sec": n_files / t_dec,
-            "png_decode_ms_per_image_one_thread": t_one * 1e3, "files": n_files, "image": [3, H, W],
-            "note": "extract_vectors (upstream scripts/test.py entry point) on %d same-size %dx%d PNG files: 16 "
-                    "decode threads, same-size chains of 64 as pinned uint8 on a copy stream; decoded = the same "
-                    "images passed as uint8 tensors (GPU-side rate incl. H2D and the D2H of the result)" % (n_files, W, H)}
+    out.update({"decoded_uint8_images_per_sec": n_files / t_dec, "files": n_files, "image": [3, H, W],
+                "decode_threads": workers,
+                "note": "extract_vectors (upstream scripts/test.py entry point) on %d same-size %dx%d PNG / JPEG "
+                        "files: %d decode threads, same-size chains of 64 as pinned uint8 on a copy stream; decoded "
+                        "= the same images passed as uint8 tensors (GPU-side rate incl. H2D and the D2H of the "
+                        "result)" % (n_files, W, H, workers)})
+    return out
 
 
 def main():

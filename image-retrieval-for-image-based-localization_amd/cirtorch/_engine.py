@@ -69,6 +69,8 @@ _SIGS = {
     "rr_local_head_workspace_bytes": ([_ll, _i, _i], _sz),
     "rr_local_head": ([_vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _vp, _i, _vp, _vp, _sz, _vp], _i),
     "rr_mutual_nn": ([_vp, _i, _vp, _i, _vp, _vp], _i),
+    "rr_rank_workspace_bytes": ([_ll, _i], _sz),
+    "rr_rank_full": ([_vp, _ll, _vp, _i, _i, _vp, _vp, _sz, _vp], _i),
     "rr_set_tuning": ([_i, _i], _i),
     "rr_fill_unit_rows": ([_vp, _ll, _i, ctypes.c_ulonglong, _ll, _vp], _i),
     "rr_cast_f32_bf16": ([_vp, _vp, _ll, _vp], _i),

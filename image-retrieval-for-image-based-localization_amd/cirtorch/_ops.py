@@ -323,6 +323,21 @@ def knn_topk(db, db_f32, q, q_f32, k, cand=0, idx_offset=0, workspace=None, db_n
     return out_s, out_i, unc
 
 
+def rank_full(db_f32, q_f32):
+    """db_f32 [n, D], q_f32 [Q, D] float32 rows (D % 256 == 0) -> int64 [Q, n]: every
+    database row per query by (float64 score desc, index asc) (rr_rank_full)."""
+    E.require_gpu(db_f32, q_f32)
+    assert db_f32.dtype == torch.float32 and q_f32.dtype == torch.float32
+    assert db_f32.is_contiguous() and q_f32.is_contiguous() and db_f32.shape[1] == q_f32.shape[1]
+    n, d = db_f32.shape
+    nq = q_f32.shape[0]
+    ws = torch.empty(int(E.lib().rr_rank_workspace_bytes(n, nq)), dtype=torch.uint8, device=db_f32.device)
+    out = torch.empty((nq, n), dtype=torch.int64, device=db_f32.device)
+    E.check(E.lib().rr_rank_full(E.ptr(db_f32), n, E.ptr(q_f32), nq, d, E.ptr(out), E.ptr(ws), ws.numel(), _st()),
+            "rr_rank_full")
+    return out
+
+
 def topk_merge(scores, idx, k):
     """scores/idx: [R, Q, k_in] per-shard lists -> merged [Q, k]."""
     E.require_gpu(scores, idx)

@@ -225,8 +225,18 @@ def _pinned_chain(slot, shape, dtype):
     return buf[:n].view(dtype).view(shape)
 
 
+def _default_workers():
+    """decode threads: the CPUs this process may run on, at most 16"""
+    import os
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
 def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], msp=1, print_freq=10,
-                    batch=64, workers=8, test_transform=None):
+                    batch=64, workers=None, test_transform=None):
     """Upstream ``extract_vectors`` (``scripts/test.py:200,236-238``): returns a
     CPU float32 tensor D x len(images).  ``images`` are file paths (PIL load,
     bbx crop, longest side resized to image_size — or ``test_transform``, an
@@ -237,10 +247,12 @@ def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], 
     Each image is extracted on its own, as with batch size 1: images are
     grouped by size (nothing is ever padded inside a group) into chains of up
     to ``batch`` images.  Windows of ``8 * batch`` inputs are decoded by
-    ``workers`` host threads while the GPU extracts the previous window;
+    ``workers`` host threads (default: the usable CPUs, at most 16) while
+    the GPU extracts the previous window;
     groups travel as pinned uint8 pixels on a copy stream double-buffered
     against the extractor (the fused stem reads x / 255)."""
     from concurrent.futures import ThreadPoolExecutor
+    workers = workers or _default_workers()
     dev = next(net.parameters()).device
     n = len(images)
     D = net.meta.get("outputdim", 2048)

@@ -4,7 +4,7 @@
 
 * ``knn(vecs, qvecs, k)``  -> first k ranks (k x Q, int64) and their scores,
   exactly ordered by (score desc, index asc); scores re-computed in float64.
-* ``rank(vecs, qvecs)``     -> full ranks (N x Q) for mAP evaluation (N <= 8192).
+* ``rank(vecs, qvecs)``     -> full ranks (N x Q) for mAP evaluation, any N.
 * ``KnnIndex``              -> a resident database (float32 rows + optional
   bf16 or fp16 screening copy) queried many times.
 * ``ShardedIndex``          -> database rows split over the ranks of a
@@ -143,11 +143,21 @@ def knn(vecs, qvecs, k, precision="fp32", cand=0):
     return i.t(), s.t()
 
 
-def rank(vecs, qvecs, precision="fp32"):
-    """Full ranking, the GPU equivalent of ``np.argsort(-np.dot(vecs.T, qvecs), axis=0)``."""
+RANK_KNN_MAX = 8192  # up to this size the top-k pipeline (LDS bitonic sort of all rows) ranks in one pass
+
+
+def rank(vecs, qvecs, precision="fp32", method="auto"):
+    """Full ranking, the GPU equivalent of ``np.argsort(-np.dot(vecs.T, qvecs), axis=0)``:
+    N x Q int64 by (score desc, index asc) on the float64 re-score.  N <= 8192: the
+    top-k pipeline with k = N; larger N (revisited datasets with distractors):
+    rr_rank_full (float64 scores + a stable radix sort), identical order."""
     n = vecs.shape[1]
-    ranks, _ = knn(vecs, qvecs, n, precision=precision, cand=n)
-    return ranks
+    if method == "knn" or (method == "auto" and n <= RANK_KNN_MAX):
+        ranks, _ = knn(vecs, qvecs, n, precision=precision, cand=n)
+        return ranks
+    db, q = _rows(vecs), _rows(qvecs)
+    d_pad = (db.shape[1] + 255) // 256 * 256
+    return _ops.rank_full(_pad_cols(db, d_pad), _pad_cols(q, d_pad)).t()
 
 
 def shard_range(n, rank, world):

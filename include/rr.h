@@ -256,6 +256,17 @@ int rr_local_head(const void* x, int n, int h, int w, int c, int dtype, const fl
  * rr_knn_topk with k = 1: exact order, ties -> lower index like np.argmin). */
 int rr_mutual_nn(const long long* nn12, int n1, const long long* nn21, int n2, long long* match, void* stream);
 
+/* Full ranking for any database size: out_idx[q][r] = the r-th database row of
+ * query q by (float64 score desc, index asc) — np.argsort(-np.dot(vecs.T, qvecs),
+ * axis=0) of scripts/test.py:247-248 as [nq][n] (rr_knn_topk ranks k <= 8192).
+ * The float64 score is rr_knn_topk's re-score (same summation order), so the
+ * first k ranks equal a top-k search.  db_f32 [n][d], q_f32 [nq][d] float32,
+ * d a multiple of 256 (zero-pad); workspace >= rr_rank_workspace_bytes
+ * (24 B x nq x n + histograms). */
+size_t rr_rank_workspace_bytes(long long n, int nq);
+int rr_rank_full(const float* db_f32, long long n, const float* q_f32, int nq, int d, long long* out_idx,
+                 void* workspace, size_t workspace_bytes, void* stream);
+
 /* ------------------------------------------------------------ tuning */
 /* Engine tuning knobs (process-wide; for benchmarking / autotuning tools):
  *   RR_TUNE_GEMM_CONFIG  0 = automatic tile choice, 1 = 128x128, 2 = 64x256,

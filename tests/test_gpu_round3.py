@@ -151,3 +151,39 @@ def test_extract_vectors_device_tensors(cuda):
     dev = extract_vectors(net, [t.to(cuda) for t in imgs], None, batch=4)
     assert torch.equal(host, dev)
 
+
+
+def _unit_rows(n, d, seed, dup_every=0):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(n, d, generator=g)
+    if dup_every:
+        x[dup_every::dup_every] = x[0]  # exact duplicates: equal float64 scores -> index order
+    return x / x.norm(dim=1, keepdim=True)
+
+
+@pytest.mark.parametrize("n,nq,d", [(20000, 7, 2048), (9000, 17, 512), (4099, 3, 256)])
+def test_rank_full_vs_numpy(cuda, n, nq, d):
+    """rr_rank_full (any N) == np.argsort of the float64 scores with ties to the lower
+    index (scripts/test.py:247-248 order, exact scores), incl. exact duplicate rows"""
+    import numpy as np
+    from cirtorch.search import rank
+    db = _unit_rows(n, d, 1, dup_every=997)
+    q = _unit_rows(nq, d, 2)
+    got = rank(db.t().to(cuda), q.t().to(cuda), method="full").cpu().numpy()
+    s = db.double().numpy() @ q.double().numpy().T               # [n, nq]
+    for j in range(nq):
+        ref = np.lexsort((np.arange(n), -s[:, j]))
+        np.testing.assert_array_equal(got[:, j], ref)
+
+
+def test_rank_full_equals_knn_pipeline(cuda):
+    """the float64 score of rr_rank_full is rr_knn_topk's re-score: at N = 8192 the two
+    full rankings are identical, and the first k of a 30000-row ranking equal top-k"""
+    from cirtorch.search import knn, rank
+    db = _unit_rows(8192, 2048, 3, dup_every=1001).t().to(cuda)
+    q = _unit_rows(9, 2048, 4).t().to(cuda)
+    assert torch.equal(rank(db, q, method="full"), rank(db, q, method="knn"))
+    db2 = _unit_rows(30000, 2048, 5, dup_every=4999).t().to(cuda)
+    r = rank(db2, q)
+    top, _ = knn(db2, q, 100)
+    assert torch.equal(r[:100], top)
