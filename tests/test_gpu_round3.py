@@ -109,10 +109,11 @@ def test_make_model_snapshot_descriptors(cuda, tmp_path, precision):
 def test_multiscale_forward_returns_loss_dict(cuda):
     from cirtorch.models.GF_net import make_net
     from cirtorch.models.init import random_init_
+    from cirtorch.utils.parallel import PackedSequence
     net = random_init_(make_net("resnet18", precision="bf16"), 1).to(cuda).eval()
     imgs = torch.rand(2, 3, 96, 128, device=cuda)
     with torch.no_grad():
-        for img in (imgs, list(imgs)):
+        for img in (imgs, PackedSequence(list(imgs))):
             loss, pred = net(img=img, scales=[0.5, 1])
             assert list(loss.keys()) == ["ret_loss"] and loss["ret_loss"] is None
             assert pred["ret_pred"].shape == (512, 2)
