@@ -18,6 +18,13 @@ __device__ __forceinline__ float powp(float x, float p, int ip) {
     return __powf(x, p);
 }
 
+// NaN-propagating clamp / max, the semantics of torch.clamp(min=eps) and
+// torch.max the reference pools use (pools.py:10-38): a NaN activation (an
+// overflowed fp16 chain) must reach the descriptor, where extract_vectors sees
+// it, instead of being replaced by eps (fmaxf drops a NaN operand).
+__device__ __forceinline__ float clamp_min_nan(float v, float eps) { return v < eps ? eps : v; }
+__device__ __forceinline__ float max_nan(float a, float b) { return (a > b || a != a) ? a : b; }
+
 // The exponent of a GeM parameter living in device memory (a learnable
 // ``pool.p``, pools.py:34) is read by the kernel itself: no host read-back, so
 // any update of the parameter (load_state_dict, optimizer step, in-place
@@ -62,8 +69,8 @@ __global__ void __launch_bounds__(256) k_pool_nhwc(const T* __restrict__ x, int 
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                if (mode == RR_POOL_GEM) acc[r] += powp(fmaxf(v[r], eps), p, ip);
-                else if (mode == RR_POOL_MAC) acc[r] = fmaxf(acc[r], v[r]);
+                if (mode == RR_POOL_GEM) acc[r] += powp(clamp_min_nan(v[r], eps), p, ip);
+                else if (mode == RR_POOL_MAC) acc[r] = max_nan(acc[r], v[r]);
                 else acc[r] += v[r];
             }
         }
@@ -77,7 +84,7 @@ __global__ void __launch_bounds__(256) k_pool_nhwc(const T* __restrict__ x, int 
             const int j = lane * 4 + r;
             float v;
             if (mode == RR_POOL_MAC) {
-                v = fmaxf(fmaxf(part[0][j], part[1][j]), fmaxf(part[2][j], part[3][j]));
+                v = max_nan(max_nan(part[0][j], part[1][j]), max_nan(part[2][j], part[3][j]));
             } else {
                 v = ((part[0][j] + part[1][j]) + (part[2][j] + part[3][j])) / (float)hw;
                 if (mode == RR_POOL_GEM) v = __powf(v, 1.0f / p);
@@ -111,11 +118,11 @@ __global__ void __launch_bounds__(1024) k_pool_nhwc_h16x8(const uint4* __restric
         for (int e = 0; e < 4; ++e) {
             const float v0 = H16<H>::lo(u[e]), v1 = H16<H>::hi(u[e]);
             if (mode == RR_POOL_GEM) {
-                acc[2 * e] += powp(fmaxf(v0, eps), p, ip);
-                acc[2 * e + 1] += powp(fmaxf(v1, eps), p, ip);
+                acc[2 * e] += powp(clamp_min_nan(v0, eps), p, ip);
+                acc[2 * e + 1] += powp(clamp_min_nan(v1, eps), p, ip);
             } else if (mac) {
-                acc[2 * e] = fmaxf(acc[2 * e], v0);
-                acc[2 * e + 1] = fmaxf(acc[2 * e + 1], v1);
+                acc[2 * e] = max_nan(acc[2 * e], v0);
+                acc[2 * e + 1] = max_nan(acc[2 * e + 1], v1);
             } else {
                 acc[2 * e] += v0;
                 acc[2 * e + 1] += v1;
@@ -139,7 +146,7 @@ __global__ void __launch_bounds__(1024) k_pool_nhwc_h16x8(const uint4* __restric
         const int ch = blockIdx.x * 512 + threadIdx.x;
         if (ch < c) {
             float v = part[0][threadIdx.x];
-            for (int w = 1; w < 16; ++w) v = mac ? fmaxf(v, part[w][threadIdx.x]) : v + part[w][threadIdx.x];
+            for (int w = 1; w < 16; ++w) v = mac ? max_nan(v, part[w][threadIdx.x]) : v + part[w][threadIdx.x];
             if (!mac) {
                 v = v / (float)hw;
                 if (mode == RR_POOL_GEM) v = __powf(v, 1.0f / p);
@@ -162,11 +169,15 @@ __global__ void __launch_bounds__(256) k_pool_nchw(const T* __restrict__ x, long
     float acc = mode == RR_POOL_MAC ? -INFINITY : 0.f;
     for (int i = lane; i < hw; i += 64) {
         float v = DT<T>::to_f(base[i]);
-        if (mode == RR_POOL_GEM) acc += powp(fmaxf(v, eps), p, ip);
-        else if (mode == RR_POOL_MAC) acc = fmaxf(acc, v);
+        if (mode == RR_POOL_GEM) acc += powp(clamp_min_nan(v, eps), p, ip);
+        else if (mode == RR_POOL_MAC) acc = max_nan(acc, v);
         else acc += v;
     }
-    acc = mode == RR_POOL_MAC ? wave_max(acc) : wave_sum(acc);
+    if (mode == RR_POOL_MAC) {
+        for (int o = 32; o > 0; o >>= 1) acc = max_nan(acc, __shfl_xor(acc, o, 64));
+    } else {
+        acc = wave_sum(acc);
+    }
     if (lane == 0) {
         float v = acc;
         if (mode != RR_POOL_MAC) {

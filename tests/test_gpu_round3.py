@@ -142,6 +142,30 @@ def test_fp16_overflow_falls_back_to_bf16(cuda):
     assert torch.isfinite(got).all() and torch.equal(got, ref)
 
 
+@pytest.mark.parametrize("layout", ["nchw", "nhwc"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+def test_pool_propagates_nan_like_torch(cuda, layout, dtype):
+    """GeM / MAC / SPoC keep a NaN activation (torch.clamp(min=eps) and max keep it,
+    pools.py:10-38): only the channel holding it is NaN, the others match torch"""
+    from cirtorch.layers import functional as LF
+    g = torch.Generator().manual_seed(3)
+    x = torch.rand(2, 64, 5, 7, generator=g).to(dtype)
+    x[1, 9, 2, 3] = float("nan")
+    x[0, 17, 4, 6] = float("nan")
+    xd = x.to(cuda)
+    if layout == "nhwc":
+        xd = xd.contiguous(memory_format=torch.channels_last)
+    xf = x.double()
+    refs = {"gem": xf.clamp(min=1e-6).pow(3).mean(dim=(2, 3)).pow(1.0 / 3),
+            "mac": xf.amax(dim=(2, 3)), "spoc": xf.mean(dim=(2, 3))}
+    for name, fn in (("gem", LF.gem), ("mac", LF.mac), ("spoc", LF.spoc)):
+        got = fn(xd).reshape(2, 64).cpu().double()
+        ref = refs[name]
+        assert torch.equal(torch.isnan(got), torch.isnan(ref)), name
+        ok = ~torch.isnan(ref)
+        assert torch.allclose(got[ok], ref[ok], rtol=1e-5, atol=1e-6), name
+
+
 def test_extract_vectors_device_tensors(cuda):
     """same-size GPU tensors are stacked on the device (no pinned host staging)"""
     from cirtorch.models.GF_net import extract_vectors, make_net
