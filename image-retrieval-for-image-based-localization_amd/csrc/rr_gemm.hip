@@ -207,7 +207,7 @@ __global__ void __launch_bounds__(64 * WC * WP, ((NS == 2 && AK * TC <= 256) || 
 
     auto issue = [&](int stage) {  // fetch step (is_tile, is_k) into `stage`, then advance
         if (is_k == 0) setup_tile(tile_at(is_tile));
-        const int k0 = is_k * BK;
+        const int k0 = tapu ? tapu_k0(is_k, a.kh * a.kw, Cin / BK, Cin, BK) : is_k * BK;
         const unsigned As = lds0 + stage * STAGE;
         const unsigned Bs = AK ? lds0 + ABYTES + stage * STAGE : As + TC * 128;
         if constexpr (AK > 0) {
@@ -215,7 +215,8 @@ __global__ void __launch_bounds__(64 * WC * WP, ((NS == 2 && AK * TC <= 256) || 
                 for (int kk = 0; kk < nk; ++kk)
 #pragma unroll
                     for (int i = 0; i < NIA; ++i) {
-                        const unsigned off = a_off[i] == OOB ? OOB : a_off[i] + (unsigned)(kk * BK * ESZ);
+                        const int kk0 = tapu ? tapu_k0(kk, a.kh * a.kw, Cin / BK, Cin, BK) : kk * BK;
+                        const unsigned off = a_off[i] == OOB ? OOB : a_off[i] + (unsigned)(kk0 * ESZ);
                         dma16(rsA, off, lds0 + kk * TC * 128 + (wave + NW * i) * 1024);
                     }
             }
@@ -683,14 +684,15 @@ __global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int n
     auto issue = [&](int X, int kt, int buf) {
         const unsigned dst = lds0 + (buf * 4 + X) * HT;
         const bool live = kt < nk;
+        const int k0 = tapu ? tapu_k0(kt, a.kh * a.kw, Cin >> 6, Cin, 64) : kt * 64;
         if (X < 2) {
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                const unsigned off = (live && a_off[X][i] != OOB) ? a_off[X][i] + (unsigned)(kt * 128) : OOB;
+                const unsigned off = (live && a_off[X][i] != OOB) ? a_off[X][i] + (unsigned)(k0 * 2) : OOB;
                 dma16(rsA, off, dst + (wave + 8 * i) * 1024);
             }
         } else {
-            const int h = X - 2, k0 = kt * 64;
+            const int h = X - 2;
             int tap_dh = 0, tap_dw = 0, tap_add = 0;
             if constexpr (tapu) {
                 const int tap = k0 >> a.lc, ci0 = k0 & (Cin - 1);
@@ -1161,14 +1163,15 @@ __global__ void __launch_bounds__(512, 1) k_gemm8a(ConvArgs a, int tiles_p, int 
     auto issue = [&](int X, int kt) {
         const unsigned dst = lds0 + (kt % 3) * ST + X * HT;
         const bool live = kt < nk;
+        const int k0 = tapu ? tapu_k0(kt, a.kh * a.kw, Cin >> 6, Cin, 64) : kt * 64;
         if (X == 0) {
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                const unsigned off = (live && a_off[i] != OOB) ? a_off[i] + (unsigned)(kt * 128) : OOB;
+                const unsigned off = (live && a_off[i] != OOB) ? a_off[i] + (unsigned)(k0 * 2) : OOB;
                 dma16(rsA, off, dst + (wave + 8 * i) * 1024);
             }
         } else {
-            const int h = X - 1, k0 = kt * 64;
+            const int h = X - 1;
             int tap_dh = 0, tap_dw = 0, tap_add = 0;
             if constexpr (tapu) {
                 const int tap = k0 >> a.lc, ci0 = k0 & (Cin - 1);

@@ -100,6 +100,19 @@ template <> struct DT<f16_t> {  // IEEE binary16, round to nearest even
     static __device__ __forceinline__ f16_t from_f(float v) { return (f16_t)v; }
 };
 
+// Packed-k offset (elements) of K-step kt of a tap-uniform im2col conv (c_in a
+// multiple of the bk-deep K-step, k = tap * c_in + ci in the packed row), in
+// (input chunk, tap) order: every conv kernel of the engine -- the direct 3x3s
+// (rr_conv3.hip / rr_conv3s.hip) and the im2col GEMMs -- accumulates a filter in
+// the same (chunk, tap, 32-channel half) order, so the kernel a layer runs on,
+// which depends on the batch size, never changes a bit of its output.  K-steps
+// past ntap * nchunk (a zero-padded k_packed tail) stay linear.
+__device__ __forceinline__ int tapu_k0(int kt, int ntap, int nchunk, int cin, int bk) {
+    if (kt >= ntap * nchunk) return kt * bk;
+    const int cc = (int)((unsigned)kt / (unsigned)ntap), tap = kt - cc * ntap;
+    return tap * cin + cc * bk;
+}
+
 // Arguments of the MFMA implicit-GEMM engine (rr_conv.hip); also drives the
 // kNN score GEMM (rr_knn.hip).
 struct ConvArgs {

@@ -747,3 +747,37 @@ def test_gemm8a_bit_identical_to_tiled_engine(cuda, shape, prec):
     ref = F.leaky_relu(ref, 0.01).permute(0, 2, 3, 1)
     err = (a[:1].cpu().double() - ref).abs().max().item()
     assert err <= 2e-2 * ref.abs().max().item(), err
+
+
+@pytest.mark.parametrize("case", [
+    (2, 256, 12, 64, 256, 3, 1, 1, False, True),   # mod4 3x3 form: direct 256-channel tiles / k_gemm8 / k_igemm
+    (1, 512, 12, 32, 512, 3, 1, 1, False, True),   # mod5 form, 8 input chunks
+    (3, 128, 16, 64, 128, 3, 1, 1, False, True),   # mod3 form: k_c3s / k_conv3x3 / k_gemm8a / k_igemm
+    (2, 256, 19, 23, 256, 3, 2, 1, False, True),   # strided 3x3: k_gemm8 / k_igemm
+    (2, 128, 18, 34, 128, 3, 2, 1, False, True),   # strided mod3 form: k_gemm8a / k_igemm
+])
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_every_3x3_path_same_bits(cuda, case, prec):
+    """All 3x3 kernels accumulate in the (input chunk, tap, 32-channel half) order,
+    so whichever the dispatcher picks for a layer (it depends on the batch size)
+    the output bits are the same: direct kernels, the 8-phase GEMMs and the tiled
+    engine on tap-uniform im2col."""
+    from cirtorch import _engine as E
+    L = E.lib()
+    outs = {}
+    # (RR_TUNE_CONV3X3, RR_TUNE_GEMM8, RR_TUNE_GRID_CUS): a CU cap of 8 makes the
+    # 8-phase kernels eligible on these small problems
+    paths = {"direct": (1, 0, 0), "gemm8": (0, 2, 8), "gemm8a": (0, 1 | 4, 8), "tiled": (0, 0, 0)}
+    try:
+        for name, (c3, g8, cap) in paths.items():
+            E.check(L.rr_set_tuning(6, c3), "rr_set_tuning")
+            E.check(L.rr_set_tuning(8, g8), "rr_set_tuning")
+            E.check(L.rr_set_tuning(7, cap), "rr_set_tuning")
+            outs[name] = _check_conv(cuda, case, prec, True)
+    finally:
+        L.rr_set_tuning(6, 1)
+        L.rr_set_tuning(8, 1)
+        L.rr_set_tuning(7, 0)
+    ref = outs.pop("tiled")
+    for name, o in outs.items():
+        assert torch.equal(o, ref), name

@@ -212,3 +212,26 @@ def test_rank_full_equals_knn_pipeline(cuda):
     r = rank(db2, q)
     top, _ = knn(db2, q, 100)
     assert torch.equal(r[:100], top)
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp16"])
+def test_batch_invariant_descriptors(cuda, precision):
+    """image 0 of an 8-image chain gets the same bits as the image alone, although
+    the kernel a layer runs on depends on the batch (CU cap 16: the mod4 / mod5 3x3s
+    take k_gemm8 at 8 images and the direct kernel at 1) -- extract_vectors' batched
+    drop-in path returns what batch 1 returns"""
+    from cirtorch import _engine as E
+    from cirtorch.models.GF_net import make_net
+    from cirtorch.models.init import random_init_
+    mean, std = [0.485, 0.456, 0.406], [0.229, 0.224, 0.225]
+    net = random_init_(make_net("resnet50", precision=precision, mean=mean, std=std), 6).to(cuda).eval()
+    g = torch.Generator().manual_seed(2)
+    x = torch.randint(0, 256, (8, 3, 768, 1024), generator=g, dtype=torch.uint8).to(cuda)
+    try:
+        E.check(E.lib().rr_set_tuning(7, 16), "rr_set_tuning")
+        with torch.no_grad():
+            many = net.extract(x)
+            one = net.extract(x[3:4].clone())
+    finally:
+        E.lib().rr_set_tuning(7, 0)
+    assert torch.equal(many[:, 3:4], one)
