@@ -491,7 +491,7 @@ def bench_dropin(net, H, W, dev, n_files=128, distinct=16):
         out = {}
         for fmt in ("png", "jpg"):
             ps = [paths[fmt][i % distinct] for i in range(n_files)]
-            extract_vectors(net, ps[:8], None, workers=workers)
+            extract_vectors(net, ps, None, workers=workers)  # warm: the pinned host blocks stay cached
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             v = extract_vectors(net, ps, None, workers=workers)
@@ -514,9 +514,10 @@ def bench_dropin(net, H, W, dev, n_files=128, distinct=16):
     out.update({"decoded_uint8_images_per_sec": n_files / t_dec, "files": n_files, "image": [3, H, W],
                 "decode_threads": workers,
                 "note": "extract_vectors (upstream scripts/test.py entry point) on %d same-size %dx%d PNG / JPEG "
-                        "files: %d decode threads, same-size chains of 64 as pinned uint8 on a copy stream; decoded "
-                        "= the same images passed as uint8 tensors (GPU-side rate incl. H2D and the D2H of the "
-                        "result)" % (n_files, W, H, workers)})
+                        "files: %d decode threads running up to 256 files ahead, decoded straight into pinned HWC "
+                        "uint8, same-size chains of 64 copied on a copy stream and transposed on the GPU (steady "
+                        "state: a warm-up call of the same size first); decoded = the same images passed as uint8 "
+                        "tensors (GPU-side rate incl. H2D and the D2H of the result)" % (n_files, W, H, workers)})
     return out
 
 

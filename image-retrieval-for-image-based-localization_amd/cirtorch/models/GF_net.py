@@ -211,6 +211,18 @@ def _decode(item, image_size, bbx, transform, tf):
     return transform(pil) if transform is not None else _to_pixels(pil)
 
 
+def _decode_pinned(item, image_size, bbx):
+    """file path -> its uint8 pixels as a pinned [H, W, 3] host tensor (the decode
+    thread's only copies: PIL's buffer and one contiguous copy into page-locked
+    memory from torch's caching host allocator, which keeps the block out of reuse
+    until the H2D copy that reads it has finished).  The HWC -> CHW transpose runs
+    on the GPU, once per chain."""
+    a = np.asarray(_load_pil(item, image_size, bbx), dtype=np.uint8)
+    t = torch.empty(a.shape, dtype=torch.uint8, pin_memory=True)
+    t.copy_(torch.from_numpy(a))
+    return t
+
+
 _PINNED = [None, None]  # one grown-on-demand pinned staging buffer per double-buffer slot, kept across calls
 
 
@@ -244,12 +256,13 @@ def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], 
     in [0, 1] or uint8 pixels).  ms/msp follow the upstream rule:
     v = (mean_s f(x_s)^msp)^(1/msp), then L2-normalised.
 
-    Each image is extracted on its own, as with batch size 1: images are
-    grouped by size (nothing is ever padded inside a group) into chains of up
-    to ``batch`` images.  Windows of ``8 * batch`` inputs are decoded by
-    ``workers`` host threads (default: the usable CPUs, at most 16) while
-    the GPU extracts the previous window;
-    groups travel as pinned uint8 pixels on a copy stream double-buffered
+    Each image is extracted on its own, as with batch size 1 (the engine's
+    kernels give the same bits whatever the chain length): images are grouped
+    by size (nothing is ever padded inside a group) into chains of up to
+    ``batch`` images.  ``workers`` host threads (default: the usable CPUs, at
+    most 16) decode up to ``4 * batch`` inputs ahead of the GPU; a chain starts
+    as soon as its group is full.  Decoded files travel as pinned uint8 HWC
+    pixels, host tensors as one pinned chain, on a copy stream double-buffered
     against the extractor (the fused stem reads x / 255)."""
     from concurrent.futures import ThreadPoolExecutor
     workers = workers or _default_workers()
@@ -273,10 +286,22 @@ def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], 
 
     outs = []  # (columns, descriptors) per chain; scattered into vecs once at the end
 
-    def run(part, items):
-        """one same-size group of images -> their descriptor columns"""
+    def run(part, items, hwc=False):
+        """one same-size group of images -> their descriptor columns (hwc: pinned
+        [H, W, 3] pixels of decoded files, copied one by one into the chain)"""
         slot = state["slot"]
-        if items[0].is_cuda:                  # device tensors: stacked in place, no host staging
+        if hwc:
+            copy.wait_event(freed[slot])
+            with torch.cuda.stream(copy):
+                xh = torch.empty((len(items),) + tuple(items[0].shape), dtype=torch.uint8, device=dev)
+                for j, t in enumerate(items):
+                    xh[j].copy_(t, non_blocking=True)
+            copied[slot].record(copy)
+            main.wait_event(copied[slot])
+            xh.record_stream(main)
+            x = xh.permute(0, 3, 1, 2).contiguous()
+            host = None
+        elif items[0].is_cuda:                # device tensors: stacked in place, no host staging
             x = torch.stack([t.to(dev) for t in items]) if len(items) > 1 else items[0].to(dev)[None]
             host = None
         elif len(part) > 1:
@@ -317,23 +342,51 @@ def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], 
     saved = net.augment
     if not normalize_in_net:
         net.augment = None
-    win = max(1, 8 * batch)
+    # Decode threads run up to `ahead` inputs in front of the consumer; decoded
+    # images are grouped by size and a group runs as soon as it holds `batch`
+    # images (partial groups: when the buffered images exceed `ahead`, the
+    # largest one runs; the rest at the end), so extraction overlaps decoding.
+    ahead = max(2, 4 * batch)
+    pinned_files = transform is None and test_transform is None
+
+    def decode(i):
+        item, bbx = images[i], bbxs[i] if bbxs is not None else None
+        if pinned_files and isinstance(item, str):
+            return "hwc", _decode_pinned(item, image_size, bbx)
+        return "chw", _decode(item, image_size, bbx, transform, test_transform)
+
     try:
         with ThreadPoolExecutor(max_workers=max(1, workers)) as pool, torch.no_grad():
-            def submit(w0):
-                return [pool.submit(_decode, images[i], image_size, bbxs[i] if bbxs is not None else None,
-                                    transform, test_transform) for i in range(w0, min(n, w0 + win))]
-            pending = submit(0)
-            for w0 in range(0, n, win):
-                decoded = [f.result() for f in pending]
-                pending = submit(w0 + win) if w0 + win < n else []
-                groups = {}
-                for j, x in enumerate(decoded):
-                    groups.setdefault((tuple(x.shape), x.dtype), []).append(j)
-                for js in groups.values():
-                    for b0 in range(0, len(js), batch):
-                        sub = js[b0:b0 + batch]
-                        run([w0 + j for j in sub], [decoded[j] for j in sub])
+            from collections import deque
+            futs = deque()
+            nxt = 0
+            groups = {}
+            buffered = 0
+
+            def flush(key):
+                nonlocal buffered
+                g = groups.pop(key)
+                buffered -= len(g)
+                run([i for i, _ in g], [x for _, x in g], hwc=key[0] == "hwc")
+
+            while nxt < n and len(futs) < ahead:
+                futs.append((nxt, pool.submit(decode, nxt)))
+                nxt += 1
+            while futs:
+                i, f = futs.popleft()
+                kind, x = f.result()
+                if nxt < n:
+                    futs.append((nxt, pool.submit(decode, nxt)))
+                    nxt += 1
+                key = (kind, tuple(x.shape), x.dtype, x.is_cuda)
+                groups.setdefault(key, []).append((i, x))
+                buffered += 1
+                if len(groups[key]) == batch:
+                    flush(key)
+                elif buffered > ahead:
+                    flush(max(groups, key=lambda k: len(groups[k])))
+            for key in list(groups):
+                flush(key)
             if outs:
                 cols = torch.tensor([c for part, _ in outs for c in part], dtype=torch.long).to(dev)
                 vecs[:, cols] = torch.cat([v for _, v in outs], dim=1)

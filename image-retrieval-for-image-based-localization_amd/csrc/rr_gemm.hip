@@ -141,6 +141,7 @@ __global__ void __launch_bounds__(64 * WC * WP, ((NS == 2 && AK * TC <= 256) || 
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wc = wave % WC, wp = wave / WC;
     const int H = a.h, W = a.w_, Cin = a.cin;
+    const float inv_ntap = 1.0f / (float)(a.kh * a.kw);  // tapu_k0
     const long long xbytes = (long long)a.n * H * W * Cin * ESZ;
     const i32x4_t rsB = make_rsrc(a.x, (unsigned)xbytes);
     const unsigned lds0 = (unsigned)(unsigned long long)smem;
@@ -207,7 +208,7 @@ __global__ void __launch_bounds__(64 * WC * WP, ((NS == 2 && AK * TC <= 256) || 
 
     auto issue = [&](int stage) {  // fetch step (is_tile, is_k) into `stage`, then advance
         if (is_k == 0) setup_tile(tile_at(is_tile));
-        const int k0 = tapu ? tapu_k0(is_k, a.kh * a.kw, Cin / BK, Cin, BK) : is_k * BK;
+        const int k0 = tapu ? tapu_k0(is_k, a.kh * a.kw, inv_ntap, Cin / BK, Cin, BK) : is_k * BK;
         const unsigned As = lds0 + stage * STAGE;
         const unsigned Bs = AK ? lds0 + ABYTES + stage * STAGE : As + TC * 128;
         if constexpr (AK > 0) {
@@ -215,7 +216,7 @@ __global__ void __launch_bounds__(64 * WC * WP, ((NS == 2 && AK * TC <= 256) || 
                 for (int kk = 0; kk < nk; ++kk)
 #pragma unroll
                     for (int i = 0; i < NIA; ++i) {
-                        const int kk0 = tapu ? tapu_k0(kk, a.kh * a.kw, Cin / BK, Cin, BK) : kk * BK;
+                        const int kk0 = tapu ? tapu_k0(kk, a.kh * a.kw, inv_ntap, Cin / BK, Cin, BK) : kk * BK;
                         const unsigned off = a_off[i] == OOB ? OOB : a_off[i] + (unsigned)(kk0 * ESZ);
                         dma16(rsA, off, lds0 + kk * TC * 128 + (wave + NW * i) * 1024);
                     }
@@ -643,6 +644,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int n
     int li = bx >> 3;  // this block's local tile index on its XCD
     if (li >= n_x) return;
     const int H = a.h, W = a.w_, Cin = a.cin;
+    const float inv_ntap = 1.0f / (float)(a.kh * a.kw);  // tapu_k0
     const int nk = a.kp / 64;
     const unsigned lds0 = (unsigned)(unsigned long long)smem;
     const int lrow = lane >> 3, lchunk = (lane & 7) ^ (lrow & 7);
@@ -684,7 +686,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int n
     auto issue = [&](int X, int kt, int buf) {
         const unsigned dst = lds0 + (buf * 4 + X) * HT;
         const bool live = kt < nk;
-        const int k0 = tapu ? tapu_k0(kt, a.kh * a.kw, Cin >> 6, Cin, 64) : kt * 64;
+        const int k0 = tapu ? tapu_k0(kt, a.kh * a.kw, inv_ntap, Cin >> 6, Cin, 64) : kt * 64;
         if (X < 2) {
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
@@ -1128,6 +1130,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm8a(ConvArgs a, int tiles_p, int 
     const int t = (xcd < rt8 ? xcd * (nt8 + 1) : rt8 * (nt8 + 1) + (xcd - rt8) * nt8) + (bx >> 3);
     if (t >= ntiles) return;
     const int H = a.h, W = a.w_, Cin = a.cin;
+    const float inv_ntap = 1.0f / (float)(a.kh * a.kw);  // tapu_k0
     const int nk = a.kp / 64;
     const unsigned lds0 = (unsigned)(unsigned long long)smem;
     const int lrow = lane >> 3, lchunk = (lane & 7) ^ (lrow & 7);
@@ -1163,7 +1166,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm8a(ConvArgs a, int tiles_p, int 
     auto issue = [&](int X, int kt) {
         const unsigned dst = lds0 + (kt % 3) * ST + X * HT;
         const bool live = kt < nk;
-        const int k0 = tapu ? tapu_k0(kt, a.kh * a.kw, Cin >> 6, Cin, 64) : kt * 64;
+        const int k0 = tapu ? tapu_k0(kt, a.kh * a.kw, inv_ntap, Cin >> 6, Cin, 64) : kt * 64;
         if (X == 0) {
 #pragma unroll
             for (int i = 0; i < 2; ++i) {

@@ -107,9 +107,12 @@ template <> struct DT<f16_t> {  // IEEE binary16, round to nearest even
 // the same (chunk, tap, 32-channel half) order, so the kernel a layer runs on,
 // which depends on the batch size, never changes a bit of its output.  K-steps
 // past ntap * nchunk (a zero-padded k_packed tail) stay linear.
-__device__ __forceinline__ int tapu_k0(int kt, int ntap, int nchunk, int cin, int bk) {
+// inv_ntap = 1 / ntap: the chunk index is (kt + 0.5) / ntap rounded down in f32
+// (exact: its fraction stays >= 0.5 / ntap away from an integer for kt < 2^16),
+// three VALU ops instead of an integer division in the DMA-issue slot.
+__device__ __forceinline__ int tapu_k0(int kt, int ntap, float inv_ntap, int nchunk, int cin, int bk) {
     if (kt >= ntap * nchunk) return kt * bk;
-    const int cc = (int)((unsigned)kt / (unsigned)ntap), tap = kt - cc * ntap;
+    const int cc = (int)(((float)kt + 0.5f) * inv_ntap), tap = kt - cc * ntap;
     return tap * cin + cc * bk;
 }
 
