@@ -141,7 +141,7 @@ __global__ void __launch_bounds__(64 * WC * WP, ((NS == 2 && AK * TC <= 256) || 
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wc = wave % WC, wp = wave / WC;
     const int H = a.h, W = a.w_, Cin = a.cin;
-    const float inv_ntap = 1.0f / (float)(a.kh * a.kw);  // tapu_k0
+    const unsigned tap_magic = tapu_magic(a.kh * a.kw);  // tapu_k0
     const long long xbytes = (long long)a.n * H * W * Cin * ESZ;
     const i32x4_t rsB = make_rsrc(a.x, (unsigned)xbytes);
     const unsigned lds0 = (unsigned)(unsigned long long)smem;
@@ -208,7 +208,7 @@ __global__ void __launch_bounds__(64 * WC * WP, ((NS == 2 && AK * TC <= 256) || 
 
     auto issue = [&](int stage) {  // fetch step (is_tile, is_k) into `stage`, then advance
         if (is_k == 0) setup_tile(tile_at(is_tile));
-        const int k0 = tapu ? tapu_k0(is_k, a.kh * a.kw, inv_ntap, Cin / BK, Cin, BK) : is_k * BK;
+        const int k0 = tapu ? tapu_k0(is_k, a.kh * a.kw, tap_magic, Cin / BK, Cin, BK) : is_k * BK;
         const unsigned As = lds0 + stage * STAGE;
         const unsigned Bs = AK ? lds0 + ABYTES + stage * STAGE : As + TC * 128;
         if constexpr (AK > 0) {
@@ -216,7 +216,7 @@ __global__ void __launch_bounds__(64 * WC * WP, ((NS == 2 && AK * TC <= 256) || 
                 for (int kk = 0; kk < nk; ++kk)
 #pragma unroll
                     for (int i = 0; i < NIA; ++i) {
-                        const int kk0 = tapu ? tapu_k0(kk, a.kh * a.kw, inv_ntap, Cin / BK, Cin, BK) : kk * BK;
+                        const int kk0 = tapu ? tapu_k0(kk, a.kh * a.kw, tap_magic, Cin / BK, Cin, BK) : kk * BK;
                         const unsigned off = a_off[i] == OOB ? OOB : a_off[i] + (unsigned)(kk0 * ESZ);
                         dma16(rsA, off, lds0 + kk * TC * 128 + (wave + NW * i) * 1024);
                     }
@@ -556,7 +556,7 @@ static void launch_ns(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
     const int ntiles = tiles_p * tiles_c;
     const int cap = PER_CU * num_cus();
     const int grid = ntiles < cap ? ntiles : cap;
-    const int km = k1 ? 1 : (a.cin * (int)sizeof(T)) % 128 == 0 ? 2 : 0;
+    const int km = k1 ? 1 : ((a.cin * (int)sizeof(T)) % 128 == 0 && tapu_ok(a.kh * a.kw, (long long)a.kp * (int)sizeof(T) / 128)) ? 2 : 0;
 #define RR_L3(PV)                                                                                                    \
     do {                                                                                                             \
         if (km == 1)                                                                                                 \
@@ -623,12 +623,24 @@ template <typename T, typename TO, int KM, bool PERM>
 __global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int ntiles) {
     static_assert(sizeof(T) == 2, "16-bit operands");
     constexpr bool K1 = KM == 1, tapu = KM == 2;
-    constexpr int VEC = 8, ESZ = 2, HT = 16384;
-    __shared__ __attribute__((aligned(1024))) char smem[8 * HT];  // [buf E/O][A0, A1, B0, B1]
+    constexpr int VEC = 8, ESZ = 2, HT = 16384, SS_MAX = 2048;
+    // [buf E/O][A0, A1, B0, B1] + folded BN scale / shift of up to 2048 channels
+    __shared__ __attribute__((aligned(1024))) char smem[8 * HT + 2 * SS_MAX * 4];
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int grp = wave >> 2;              // wave group; also the 64-row half of each quadrant
+    // The epilogue reads scale / shift from LDS, so it issues no global load: a
+    // load there would wait (vmcnt is in order) for the next tile's prologue DMA.
+    float* const lds_sc = reinterpret_cast<float*>(smem + 8 * HT);
+    float* const lds_sh = lds_sc + SS_MAX;
+    const bool ss_lds = PERM && (a.flags & RR_CONV_AFFINE) && a.cout <= SS_MAX;
+    if (ss_lds) {
+        for (int c = tid; c < a.cout; c += 512) {
+            lds_sc[c] = a.scale[c];
+            lds_sh[c] = a.shift[c];
+        }
+    }
     const int wn = wave & 3;                // 32-column quarter of each quadrant
     // XCD-contiguous bijective tile order (blocks are dispatched round-robin over 8 XCDs)
     // Persistent blocks over an XCD-contiguous tile order: XCD x (blocks are
@@ -644,7 +656,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int n
     int li = bx >> 3;  // this block's local tile index on its XCD
     if (li >= n_x) return;
     const int H = a.h, W = a.w_, Cin = a.cin;
-    const float inv_ntap = 1.0f / (float)(a.kh * a.kw);  // tapu_k0
+    const unsigned tap_magic = tapu_magic(a.kh * a.kw);  // tapu_k0
     const int nk = a.kp / 64;
     const unsigned lds0 = (unsigned)(unsigned long long)smem;
     const int lrow = lane >> 3, lchunk = (lane & 7) ^ (lrow & 7);
@@ -682,43 +694,57 @@ __global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int n
             }
     };
     setup(s_x + li);
-    // half-tile X (0 A0, 1 A1, 2 B0, 3 B1) of K-step kt into buffer buf; K-steps >= nk load zeros
-    auto issue = [&](int X, int kt, int buf) {
+    // K-step descriptor, computed once per K-step (not per half-tile issue): the
+    // DMA-issue slots sit between the barriers of the staggered schedule, so
+    // every instruction there delays the partner group's matrix pipe.  The tap
+    // split uses magic multiplies (no integer division on the issue path).
+    const unsigned kw_magic = tapu_magic(a.kw);
+    struct KD {
+        int k0, dh, dw, add;
+        bool live;
+    };
+    auto kdesc = [&](int kt) {
+        KD d;
+        d.live = kt < nk;
+        d.k0 = tapu ? tapu_k0(kt, a.kh * a.kw, tap_magic, Cin >> 6, Cin, 64) : kt * 64;
+        d.dh = d.dw = d.add = 0;
+        if constexpr (tapu) {
+            const int tap = d.k0 >> a.lc, ci0 = d.k0 & (Cin - 1);
+            const int kh = (int)(((unsigned)tap * kw_magic) >> 16), kw = tap - kh * a.kw;
+            d.dh = kh * a.dil;
+            d.dw = kw * a.dil;
+            d.add = (d.dh * W + d.dw) * Cin + ci0;
+        }
+        return d;
+    };
+    // half-tile X (0 A0, 1 A1, 2 B0, 3 B1) of K-step d into buffer buf; K-steps >= nk load zeros
+    auto issue = [&](int X, const KD& d, int buf) {
         const unsigned dst = lds0 + (buf * 4 + X) * HT;
-        const bool live = kt < nk;
-        const int k0 = tapu ? tapu_k0(kt, a.kh * a.kw, inv_ntap, Cin >> 6, Cin, 64) : kt * 64;
         if (X < 2) {
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                const unsigned off = (live && a_off[X][i] != OOB) ? a_off[X][i] + (unsigned)(k0 * 2) : OOB;
+                const unsigned off = (d.live && a_off[X][i] != OOB) ? a_off[X][i] + (unsigned)(d.k0 * 2) : OOB;
                 dma16(rsA, off, dst + (wave + 8 * i) * 1024);
             }
         } else {
             const int h = X - 2;
-            int tap_dh = 0, tap_dw = 0, tap_add = 0;
-            if constexpr (tapu) {
-                const int tap = k0 >> a.lc, ci0 = k0 & (Cin - 1);
-                const int kh = tap / a.kw, kw = tap - kh * a.kw;
-                tap_dh = kh * a.dil;
-                tap_dw = kw * a.dil;
-                tap_add = (tap_dh * W + tap_dw) * Cin + ci0;
-            }
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 unsigned off = OOB;
-                if (live && b_base[h][i] != OOB) {
+                if (d.live && b_base[h][i] != OOB) {
                     if constexpr (K1) {
-                        off = (b_base[h][i] + (unsigned)k0) * ESZ;
+                        off = (b_base[h][i] + (unsigned)d.k0) * ESZ;
                     } else {
-                        const int hi = b_hi[h][i] + tap_dh, wi = b_wi[h][i] + tap_dw;
+                        const int hi = b_hi[h][i] + d.dh, wi = b_wi[h][i] + d.dw;
                         if ((unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W)
-                            off = (b_base[h][i] + (unsigned)tap_add) * ESZ;
+                            off = (b_base[h][i] + (unsigned)d.add) * ESZ;
                     }
                 }
                 dma16(rsB, off, dst + (wave + 8 * i) * 1024);
             }
         }
     };
+    const KD kd0 = kdesc(0), kd1 = kdesc(1);
 
     f32x4_t acc[2][2][4][2];
 #pragma unroll
@@ -773,45 +799,55 @@ __global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int n
 
     // ---- prologue: K-step 0 into E (A0 B1 A1 B0), K-step 1's A0 / B1 into O
     auto prologue = [&]() {
-        issue(0, 0, 0);
-        issue(3, 0, 0);
-        issue(1, 0, 0);
-        issue(2, 0, 0);
-        issue(0, 1, 1);
-        issue(3, 1, 1);
+        issue(0, kd0, 0);
+        issue(3, kd0, 0);
+        issue(1, kd0, 0);
+        issue(2, kd0, 0);
+        issue(0, kd1, 1);
+        issue(3, kd1, 1);
     };
     prologue();
     const int nit = (nk + 1) >> 1;
+    // the previous tile's epilogue issued exactly ST_FULL stores and nothing else
+    // (a full tile, no residual load); they are younger than this tile's prologue
+    constexpr int ST_FULL = 16;
+    static_assert(4 + ST_FULL == 20, "the counted wait below");
+    bool prev_full = false;
     for (;;) {
-        // K-step 0 has landed: only the 4 youngest VMEM ops may still be in flight
-        // (K-step 1's A0 / B1, or the previous tile's last epilogue stores, which
-        // were issued after this tile's prologue)
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        // K-step 0 has landed: only the 4 youngest DMAs (K-step 1's A0 / B1) and
+        // the previous tile's epilogue stores (issued after this tile's prologue)
+        // may still be in flight; an epilogue with a data-dependent store count
+        // is waited for entirely
+        if (prev_full) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");  // 4 + ST_FULL
+        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         bar();
         if (grp == 1) bar();  // stagger: group 1 runs one barrier behind group 0
 
+    KD dto = kd1;  // descriptor of K-step `to`, carried from the previous iteration's to + 2
     for (int it = 0; it < nit; ++it) {
         const int te = 2 * it, to = 2 * it + 1;
+        const KD de2 = kdesc(te + 2), do2 = kdesc(to + 2);
         // phases 1-4: K-step te from E; loads: A1-O(to), B0-O(to), A0-E(te+2), B1-E(te+2)
-        read_a(0, 0); read_b(0, 0); issue(1, to, 1);
+        read_a(0, 0); read_b(0, 0); issue(1, dto, 1);
         bar(); mfma_q(0, 0); bar();
-        read_b(0, 1); issue(2, to, 1);
+        read_b(0, 1); issue(2, dto, 1);
         bar(); mfma_q(0, 1); bar();
-        read_a(0, 1); issue(0, te + 2, 0);
+        read_a(0, 1); issue(0, de2, 0);
         bar(); mfma_q(1, 1); bar();
-        read_b(0, 0); issue(3, te + 2, 0);
+        read_b(0, 0); issue(3, de2, 0);
         asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // K-step `to` (buffer O) has landed
         bar(); mfma_q(1, 0); bar();
         // phases 5-8: K-step to from O; loads: A1-E(te+2), B0-E(te+2), A0-O(to+2), B1-O(to+2)
-        read_a(1, 0); read_b(1, 0); issue(1, te + 2, 0);
+        read_a(1, 0); read_b(1, 0); issue(1, de2, 0);
         bar(); mfma_q(0, 0); bar();
-        read_b(1, 1); issue(2, te + 2, 0);
+        read_b(1, 1); issue(2, de2, 0);
         bar(); mfma_q(0, 1); bar();
-        read_a(1, 1); issue(0, to + 2, 1);
+        read_a(1, 1); issue(0, do2, 1);
         bar(); mfma_q(1, 1); bar();
-        read_b(1, 0); issue(3, to + 2, 1);
+        read_b(1, 0); issue(3, do2, 1);
         asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // K-step te + 2 (buffer E) has landed
         bar(); mfma_q(1, 0); bar();
+        dto = do2;
     }
     if (grp == 0) bar();  // equal barrier counts for both groups: every wave's LDS reads are done
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing (zero) K-step DMAs have landed
@@ -830,6 +866,8 @@ __global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int n
     const bool affine = a.flags & RR_CONV_AFFINE;
     const bool resid = a.flags & RR_CONV_RESIDUAL;
     const bool leaky = a.act == RR_ACT_LEAKY;
+    if constexpr (PERM && sizeof(TO) == 2)
+        prev_full = !resid && (ss_lds || !affine) && ec0 + 256 <= a.cout && ep0 + 256 <= a.P;
 #pragma unroll
     for (int qa = 0; qa < 2; ++qa) {
         if constexpr (PERM) {
@@ -838,7 +876,10 @@ __global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int n
                 const int c = ec0 + qa * 128 + grp * 64 + 32 * i2 + 8 * kq;  // 8 consecutive channels
                 if (c >= a.cout) continue;
                 float sc[8], sh[8];
-                if (affine) {
+                if (ss_lds) {
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) { sc[r] = lds_sc[c + r]; sh[r] = lds_sh[c + r]; }
+                } else if (affine) {
                     St4<float>::ld(a.scale + c, sc);
                     St4<float>::ld(a.scale + c + 4, sc + 4);
                     St4<float>::ld(a.shift + c, sh);
@@ -1130,7 +1171,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm8a(ConvArgs a, int tiles_p, int 
     const int t = (xcd < rt8 ? xcd * (nt8 + 1) : rt8 * (nt8 + 1) + (xcd - rt8) * nt8) + (bx >> 3);
     if (t >= ntiles) return;
     const int H = a.h, W = a.w_, Cin = a.cin;
-    const float inv_ntap = 1.0f / (float)(a.kh * a.kw);  // tapu_k0
+    const unsigned tap_magic = tapu_magic(a.kh * a.kw);  // tapu_k0
     const int nk = a.kp / 64;
     const unsigned lds0 = (unsigned)(unsigned long long)smem;
     const int lrow = lane >> 3, lchunk = (lane & 7) ^ (lrow & 7);
@@ -1162,37 +1203,48 @@ __global__ void __launch_bounds__(512, 1) k_gemm8a(ConvArgs a, int tiles_p, int 
             }
         }
     }
-    // half-tile X (0 A0, 1 B0, 2 B1) of K-step kt into its ring stage; K-steps >= nk load zeros
-    auto issue = [&](int X, int kt) {
-        const unsigned dst = lds0 + (kt % 3) * ST + X * HT;
-        const bool live = kt < nk;
-        const int k0 = tapu ? tapu_k0(kt, a.kh * a.kw, inv_ntap, Cin >> 6, Cin, 64) : kt * 64;
+    // K-step descriptor, once per K-step (k_gemm8's KD: no division on the issue path)
+    const unsigned kw_magic = tapu_magic(a.kw);
+    struct KD {
+        int k0, dh, dw, add, stage;
+        bool live;
+    };
+    auto kdesc = [&](int kt) {
+        KD d;
+        d.live = kt < nk;
+        d.stage = kt % 3;
+        d.k0 = tapu ? tapu_k0(kt, a.kh * a.kw, tap_magic, Cin >> 6, Cin, 64) : kt * 64;
+        d.dh = d.dw = d.add = 0;
+        if constexpr (tapu) {
+            const int tap = d.k0 >> a.lc, ci0 = d.k0 & (Cin - 1);
+            const int kh = (int)(((unsigned)tap * kw_magic) >> 16), kw = tap - kh * a.kw;
+            d.dh = kh * a.dil;
+            d.dw = kw * a.dil;
+            d.add = (d.dh * W + d.dw) * Cin + ci0;
+        }
+        return d;
+    };
+    // half-tile X (0 A0, 1 B0, 2 B1) of K-step d into its ring stage; K-steps >= nk load zeros
+    auto issue = [&](int X, const KD& d) {
+        const unsigned dst = lds0 + d.stage * ST + X * HT;
         if (X == 0) {
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                const unsigned off = (live && a_off[i] != OOB) ? a_off[i] + (unsigned)(k0 * 2) : OOB;
+                const unsigned off = (d.live && a_off[i] != OOB) ? a_off[i] + (unsigned)(d.k0 * 2) : OOB;
                 dma16(rsA, off, dst + (wave + 8 * i) * 1024);
             }
         } else {
             const int h = X - 1;
-            int tap_dh = 0, tap_dw = 0, tap_add = 0;
-            if constexpr (tapu) {
-                const int tap = k0 >> a.lc, ci0 = k0 & (Cin - 1);
-                const int kh = tap / a.kw, kw = tap - kh * a.kw;
-                tap_dh = kh * a.dil;
-                tap_dw = kw * a.dil;
-                tap_add = (tap_dh * W + tap_dw) * Cin + ci0;
-            }
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 unsigned off = OOB;
-                if (live && b_base[h][i] != OOB) {
+                if (d.live && b_base[h][i] != OOB) {
                     if constexpr (K1) {
-                        off = (b_base[h][i] + (unsigned)k0) * ESZ;
+                        off = (b_base[h][i] + (unsigned)d.k0) * ESZ;
                     } else {
-                        const int hi = b_hi[h][i] + tap_dh, wi = b_wi[h][i] + tap_dw;
+                        const int hi = b_hi[h][i] + d.dh, wi = b_wi[h][i] + d.dw;
                         if ((unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W)
-                            off = (b_base[h][i] + (unsigned)tap_add) * ESZ;
+                            off = (b_base[h][i] + (unsigned)d.add) * ESZ;
                     }
                 }
                 dma16(rsB, off, dst + (wave + 8 * i) * 1024);
@@ -1248,20 +1300,24 @@ __global__ void __launch_bounds__(512, 1) k_gemm8a(ConvArgs a, int tiles_p, int 
     };
     auto bar = []() { asm volatile("s_barrier" ::: "memory"); };
 
-    issue(0, 0); issue(1, 0); issue(2, 0);
-    issue(0, 1); issue(1, 1); issue(2, 1);
+    {
+        const KD d0 = kdesc(0), d1 = kdesc(1);
+        issue(0, d0); issue(1, d0); issue(2, d0);
+        issue(0, d1); issue(1, d1); issue(2, d1);
+    }
     asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // K-step 0's A0 / B0
     bar();
     if (grp == 1) bar();
     for (int kt = 0; kt < nk; ++kt) {
+        const KD d2 = kdesc(kt + 2);
         // phase A: A0 x B0 of K-step kt; K-step kt + 2's A0 / B0
         read_a(kt); read_b(kt, 0);
-        issue(0, kt + 2); issue(1, kt + 2);
+        issue(0, d2); issue(1, d2);
         asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // K-step kt's B1 has landed
         bar(); mfma_q(0); bar();
         // phase B: A0 (registers) x B1; K-step kt + 2's B1
         read_b(kt, 1);
-        issue(2, kt + 2);
+        issue(2, d2);
         asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // K-step kt + 1's A0 / B0 have landed
         bar(); mfma_q(1); bar();
     }
@@ -1335,7 +1391,7 @@ bool gemm8_eligible(const ConvArgs& a, bool k1, int esz) {
         g_gemm8 = (e && e[0] == '0') ? 0 : 1;
     }
     if (!g_gemm8 || esz != 2) return false;
-    const int km = k1 ? 1 : (a.cin * 2) % 128 == 0 ? 2 : 0;
+    const int km = k1 ? 1 : ((a.cin * 2) % 128 == 0 && tapu_ok(a.kh * a.kw, a.kp / 64)) ? 2 : 0;
     const int nk = a.kp / 64;
     if (km == 0 || nk < 2 || (nk & 1) || a.kp % 64) return false;
     if ((long long)a.n * a.h * a.w_ * a.cin * 2 >= (1ll << 31) || 256ll * a.kp * 2 >= (1ll << 31)) return false;
@@ -1407,7 +1463,7 @@ static int g_gemm8a = 1;  // rr_set_tuning(RR_TUNE_GEMM8, value | 16): k_gemm8a 
 // tap-uniform im2col), enough 128 x 256 tiles to fill the chip twice.
 bool gemm8a_eligible(const ConvArgs& a, bool k1) {
     if (!g_gemm8a || !(a.flags & RR_CONV_PERM32) || a.cout % 128 || a.cout >= 256) return false;
-    const int km = k1 ? 1 : (a.cin * 2) % 128 == 0 ? 2 : 0;
+    const int km = k1 ? 1 : ((a.cin * 2) % 128 == 0 && tapu_ok(a.kh * a.kw, a.kp / 64)) ? 2 : 0;
     if (km == 0 || a.kp % 64 || a.kp / 64 < 2) return false;
     if ((long long)a.n * a.h * a.w_ * a.cin * 2 >= (1ll << 31) || 128ll * a.kp * 2 >= (1ll << 31)) return false;
     const long long ntiles = (long long)((a.P + 255) / 256) * (a.cout / 128);

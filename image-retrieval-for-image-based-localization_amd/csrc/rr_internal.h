@@ -107,12 +107,18 @@ template <> struct DT<f16_t> {  // IEEE binary16, round to nearest even
 // the same (chunk, tap, 32-channel half) order, so the kernel a layer runs on,
 // which depends on the batch size, never changes a bit of its output.  K-steps
 // past ntap * nchunk (a zero-padded k_packed tail) stay linear.
-// inv_ntap = 1 / ntap: the chunk index is (kt + 0.5) / ntap rounded down in f32
-// (exact: its fraction stays >= 0.5 / ntap away from an integer for kt < 2^16),
-// three VALU ops instead of an integer division in the DMA-issue slot.
-__device__ __forceinline__ int tapu_k0(int kt, int ntap, float inv_ntap, int nchunk, int cin, int bk) {
+// magic = ceil(2^16 / ntap): the chunk index (kt * magic) >> 16 equals
+// kt / ntap for every kt < 2^16 / ntap (checked on the host: tapu_ok), two
+// scalar integer instructions on the DMA issue path instead of a division.
+__host__ __device__ __forceinline__ unsigned tapu_magic(int ntap) { return (65536u + (unsigned)ntap - 1u) / (unsigned)ntap; }
+// every K-step index of a conv with ntap taps and nsteps tap-uniform K-steps is in that range
+__host__ __device__ __forceinline__ bool tapu_ok(int ntap, long long nsteps) { return nsteps * (ntap - 1) < 65536; }
+__device__ __forceinline__ int tapu_k0(int kt, int ntap, unsigned magic, int nchunk, int cin, int bk) {
+#ifdef RR_TAPU_LINEAR  // timing experiments only: the linear (tap, chunk) order
+    return kt * bk;
+#endif
     if (kt >= ntap * nchunk) return kt * bk;
-    const int cc = (int)(((float)kt + 0.5f) * inv_ntap), tap = kt - cc * ntap;
+    const int cc = (int)(((unsigned)kt * magic) >> 16), tap = kt - cc * ntap;
     return tap * cin + cc * bk;
 }
 

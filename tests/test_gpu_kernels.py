@@ -679,13 +679,15 @@ def test_gemm8_residual_epilogue_bit_identical(cuda, shape, leaky, prec):
 
 
 @pytest.mark.parametrize("cap", [0, 9, 37])
+@pytest.mark.parametrize("resid", [True, False])
 @pytest.mark.parametrize("shape", [(16, 48, 64, 1024, 256, 1, 1), (16, 24, 32, 512, 2048, 1, 1),
-                                   (16, 48, 64, 256, 256, 3, 1)])
-def test_gemm8_persistent_equals_one_block_per_tile(cuda, shape, cap):
+                                   (16, 48, 64, 256, 256, 3, 1), (5, 19, 29, 512, 256, 1, 1)])
+def test_gemm8_persistent_equals_one_block_per_tile(cuda, shape, cap, resid):
     """Persistent k_gemm8 blocks (each walks its XCD's tile range, the next tile's
     prologue DMA overlapping the epilogue) vs one block per tile (RR_TUNE_GEMM8 | 4):
-    bit-identical, also with grid caps that give the XCDs unequal block counts and
-    a residual epilogue."""
+    bit-identical, also with grid caps that give the XCDs unequal block counts, a
+    residual epilogue, and ragged pixel tiles between full ones (the counted wait
+    after a full tile's 16 epilogue stores vs the full drain after a partial one)."""
     from cirtorch import _engine as E
     n, h, w, cin, cout, k, s = shape
     g = torch.Generator(device=cuda).manual_seed(11)
@@ -695,7 +697,9 @@ def test_gemm8_persistent_equals_one_block_per_tile(cuda, shape, cap):
     sc = torch.rand(cout, generator=g, device=cuda) + 0.5
     sh = torch.randn(cout, generator=g, device=cuda) * 0.1
     p = 1 if k == 3 else 0
-    res = torch.randn((n, h, w, cout), generator=g, device=cuda).to(torch.bfloat16) if k == 1 else None
+    if resid and k != 1:
+        pytest.skip("residual epilogues are 1x1s")
+    res = torch.randn((n, h, w, cout), generator=g, device=cuda).to(torch.bfloat16) if resid else None
     E.check(E.lib().rr_set_tuning(6, 0), "rr_set_tuning")
     E.check(E.lib().rr_set_tuning(5, 0), "rr_set_tuning")
     try:

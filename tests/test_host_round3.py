@@ -173,3 +173,38 @@ def test_map_ignores_minus_one_padding(as_tensor):
         assert got[0] == ref[0]
         np.testing.assert_array_equal(got[1], ref[1])
         np.testing.assert_array_equal(got[3], ref[3])
+
+
+def test_process_decoder_ring_matches_thread_loader(tmp_path):
+    """extract_vectors' process decoder (cirtorch/utils/decode_procs.py): every
+    file decodes into its shared-memory slot with the same bytes as the thread
+    path's PIL loader (GF_net._load_pil: RGB, bbx crop, thumbnail); an image
+    larger than a slot comes back pickled; released slots are reused."""
+    import numpy as np
+    from PIL import Image
+    from cirtorch.models.GF_net import _load_pil
+    from cirtorch.utils.decode_procs import ProcDecoder
+    r = np.random.default_rng(0)
+    paths = []
+    for i, (h, w) in enumerate([(40, 52), (61, 33), (90, 120), (12, 8)]):
+        a = (r.random((h, w, 3)) * 255).astype(np.uint8)
+        p = str(tmp_path / ("%d.%s" % (i, "png" if i % 2 else "jpg")))
+        Image.fromarray(a).save(p)
+        paths.append(p)
+    d = ProcDecoder(2, 3, slot_bytes=64 * 64 * 3)
+    try:
+        for bbx, imsize in [(None, None), ((2, 3, 30, 11), None), (None, 24)]:
+            pend = [d.submit(p, imsize, bbx) for p in paths[:3]]
+            outs = [q.result() for q in pend]
+            for p, t in zip(paths, outs):
+                ref = np.asarray(_load_pil(p, imsize, bbx), dtype=np.uint8)
+                assert t.shape == ref.shape and (t.numpy() == ref).all(), (p, bbx, imsize)
+            # hand the ring views back (an event that has completed: a CPU stand-in)
+            class Done:
+                def query(self):
+                    return True
+            d.release(outs, Done())
+        big = d.submit(paths[2], None, None).result()      # 90 x 120 x 3 > one slot
+        assert not d.owns(big) and big.shape == (90, 120, 3)
+    finally:
+        d.close()

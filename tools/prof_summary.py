@@ -11,7 +11,7 @@ import csv
 import json
 
 BODY = ("k_stem_pool", "k_conv3x3", "k_stream1x1", "k_stream_pair", "k_igemm<unsigned short, unsigned short",
-        "k_gemm8<unsigned short, unsigned short", "k_pair_mid", "k_gemm8a<")
+        "k_gemm8<unsigned short, unsigned short", "k_pair_mid", "k_gemm8a<", "k_c3s_w")
 
 
 def main():
@@ -29,7 +29,8 @@ def main():
         print("| %.2f | %.1f | %s | %.1f | `%s` |" % (100 * float(r["TotalDurationNs"]) / tot,
                                                     float(r["TotalDurationNs"]) / 1e3, r["Calls"],
                                                     float(r["AverageNs"]) / 1e3, r["Name"][:120]))
-    body = [r for r in rows if any(k in r["Name"] for k in BODY)]
+    # the bf16 headline forwards only (the fp16 e2e line's kernels carry mangled DF16_ names)
+    body = [r for r in rows if any(k in r["Name"] for k in BODY) and "DF16_" not in r["Name"]]
     body_us = sum(float(r["TotalDurationNs"]) for r in body) / 1e3 / args.forwards
     eb = b["config"].get("extract_batch", b["config"]["global_batch"])
     per_fwd_bench = b["roofline"]["achieved"] and (b["roofline_layers"]["measured_ms"] * 1e3 *

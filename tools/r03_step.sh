@@ -53,7 +53,7 @@ d=json.loads(open('$OUT/benchenv_$i.json').read().strip().splitlines()[-1]); pri
       tail -3 "$OUT/pytest_gpu.log" ;;
     prof)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run \
-        --output-format csv -- python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --no-extras --latency 0 --pcie-steps 0 \
+        --output-format csv -- python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --no-extras --latency 0 --pcie-steps 0 --fp16-steps 0 \
         > "$OUT/prof_bench.json" 2> "$OUT/prof.err") || { tail -20 "$OUT/prof.err"; exit 1; }
       tail -c 1500 "$OUT/prof_bench.json" ;;
     *) echo "unknown step $STEP"; exit 2 ;;
