@@ -740,6 +740,25 @@ def main():
                    "roofline": {"bound": "mfma", "achieved": flops / tk / 1e12, "peak": peak, "unit": "TFLOP/s",
                                 "frac": flops / tk / 1e12 / peak, "traffic": None,
                                 "note": "per-rank screening GEMM FLOPs 2*Q*n_local*D / whole search time"}}
+            # the step's own search alone (B x world queries, no extraction beside it):
+            # at <= 128 queries the score GEMM streams the screening copy of the DB
+            qs1 = _ops.fill_unit_rows(B * world, args.dim, seed=0x0E5EED + 1, row0=0, device=dev)
+            index.search(qs1, args.k)
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            t3 = time.perf_counter()
+            for _ in range(args.knn_steps):
+                index.search(qs1, args.k)
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            ts = max_over_ranks((time.perf_counter() - t3) / args.knn_steps)
+            db_bytes = float(n_local) * args.dim * (4 if args.precision == "fp32" else 2)
+            knn["step_search"] = {"q": B * world, "ms_per_search": ts * 1e3, "queries_per_sec": B * world / ts,
+                                  "roofline": {"bound": "hbm", "achieved": db_bytes / ts / 1e9, "peak": PEAK_HBM_GBS,
+                                               "unit": "GB/s", "frac": db_bytes / ts / 1e9 / PEAK_HBM_GBS,
+                                               "note": "screening-copy DB bytes per rank / whole search time"}}
             kt, kpath, kfresh = pmc_file("knn_q%d" % args.knn_q, lambda c: (
                 c.get("db_rows"), c.get("dim"), c.get("k"), c.get("screen")) == (
                 args.db_rows, args.dim, args.k, args.precision))

@@ -245,12 +245,8 @@ class _PinnedBlocks:
         n = int(np.prod(shape))
         with self.lock:
             self._reclaim()
-            fit = [b for b in self.free if b.numel() >= n]
-            if fit:
-                b = min(fit, key=lambda t: t.numel())
-                self.free.remove(b)
-            else:
-                b = None
+            fit = [k for k, b in enumerate(self.free) if b.numel() >= n]
+            b = self.free.pop(min(fit, key=lambda k: self.free[k].numel())) if fit else None
         if b is None:
             b = torch.empty(n, dtype=torch.uint8, pin_memory=True)
         v = b[:n].view(shape)

@@ -856,16 +856,16 @@ __global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int n
     const int ec0 = c0, ep0 = p0;
     li += nb_x;
     const bool more = li < n_x;
-    if (more) {
-        setup(s_x + li);
-        prologue();
-    }
-    // ---- epilogue: folded BN scale / shift, residual, activation, NHWC store
     TO* __restrict__ Y = (TO*)a.y;
     const TO* __restrict__ R = (const TO*)a.res;
     const bool affine = a.flags & RR_CONV_AFFINE;
     const bool resid = a.flags & RR_CONV_RESIDUAL;
     const bool leaky = a.act == RR_ACT_LEAKY;
+    if (more) {
+        setup(s_x + li);
+        prologue();
+    }
+    // ---- epilogue: folded BN scale / shift, residual, activation, NHWC store
     if constexpr (PERM && sizeof(TO) == 2)
         prev_full = !resid && (ss_lds || !affine) && ec0 + 256 <= a.cout && ep0 + 256 <= a.P;
 #pragma unroll
@@ -1148,6 +1148,168 @@ __global__ void __launch_bounds__(512, 1) k_gemm8h(ConvArgs a, int ntiles) {
 }
 
 // ---------------------------------------------------------------------------
+// Streaming form of the <= 128-query kNN score GEMM (k_gemm8s).  At 128 queries
+// a DB byte feeds only 128 MACs, so k_gemm8h is bound by how many DB bytes it
+// keeps in flight, and its LDS ring (3 stages x 48 KiB) gives a DMA only about
+// two K-steps (~1 us) to land.  Here the DB rows bypass LDS: each wave owns 32
+// rows of a 256-row tile and loads their A fragments straight into registers,
+// R K-steps ahead (R x 4 KiB per wave, 8 x R x 4 KiB per CU in flight); only the
+// queries -- shared by all 8 waves -- go through an LDS ring of R + 1 K-steps
+// (16 KiB each, LDS-DMA).  Blocks are persistent over an XCD-contiguous tile
+// range and the K-step stream runs on across tiles, so the next tile's rows are
+// already in flight during a tile's epilogue.  Per element the MFMA operands, K
+// order and accumulation order are k_gemm8h's (16x16x32, K-steps in order, the
+// two 32-deep halves in order), so the scores -- and k_slot_fixup's recomputed
+// keys -- are bit-identical to it.
+// vmcnt: per stream position the block issues 2 query DMAs (asm, not counted
+// by the compiler) and then 4 DB loads (compiler-visible); position f's query
+// stage is complete once at most 6 (R - 1) + 4 younger operations remain.
+template <typename T, int R>
+__global__ void __launch_bounds__(512, 1) k_gemm8s(ConvArgs a, int ntiles) {
+    static_assert(sizeof(T) == 2 && 6 * (R - 1) + 4 <= 63, "16-bit operands, vmcnt range");
+    constexpr int ESZ = 2, HT = 16384, NB = R + 1;
+    __shared__ __attribute__((aligned(1024))) char smem[NB * HT];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nwg = (int)gridDim.x, bx = (int)blockIdx.x, xcd = bx & 7;
+    const int nt8 = ntiles >> 3, rt8 = ntiles & 7;
+    const int s_x = xcd < rt8 ? xcd * (nt8 + 1) : rt8 * (nt8 + 1) + (xcd - rt8) * nt8;
+    const int n_x = nt8 + (xcd < rt8 ? 1 : 0);
+    const int nb_x = (nwg >> 3) + (xcd < (nwg & 7) ? 1 : 0);
+    const int li = bx >> 3;
+    if (li >= n_x) return;
+    const int my = (n_x - li + nb_x - 1) / nb_x;  // tiles of this block: s_x + li + m * nb_x
+    const int nk = a.kp / 64;
+    const int F = my * nk;                        // (tile, K-step) stream of this block
+    const unsigned lds0 = (unsigned)(unsigned long long)smem;
+    const int lrow = lane >> 3, lchunk = (lane & 7) ^ (lrow & 7);
+    const int r16 = lane & 15, kq = lane >> 4;
+
+    const i32x4_t rsB = make_rsrc(a.x, (unsigned)((long long)a.P * a.cin * ESZ));
+    unsigned b_off[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int p = (wave + 8 * i) * 8 + lrow;
+        b_off[i] = p < a.P ? (unsigned)(((long long)p * a.cin + lchunk * 8) * ESZ) : OOB;
+    }
+    // issue side: stream position (mi, ki); this lane's two DB rows of tile mi
+    // (positions past the block's stream re-read its last tile: same count of
+    // operations in flight, results unused)
+    int mi = 0, ki = 0;
+    const char* arow[2];
+    auto set_rows = [&](int m) {
+        const int t = s_x + li + min(m, my - 1) * nb_x;
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            const int row = min(t * 256 + 32 * wave + 16 * g + r16, a.cout - 1);
+            arow[g] = (const char*)a.w + (long long)row * a.kp * ESZ + kq * 16;
+        }
+    };
+    set_rows(0);
+    uint4 ar[R][2][2];  // [ring slot][row group][32-deep half]
+    int bst = 0;        // query stage of the next issue
+    auto issue = [&](uint4 (&dst)[2][2]) {
+        const bool live = mi < my;
+        const unsigned dstl = lds0 + bst * HT;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            dma16(rsB, (live && b_off[i] != OOB) ? b_off[i] + (unsigned)(ki * 128) : OOB, dstl + (wave + 8 * i) * 1024);
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+#pragma unroll
+            for (int hs = 0; hs < 2; ++hs)
+                dst[g][hs] = *reinterpret_cast<const uint4*>(arow[g] + ki * 128 + hs * 64);
+        bst = bst + 1 == NB ? 0 : bst + 1;
+        if (++ki == nk) {
+            ki = 0;
+            ++mi;
+            set_rows(mi);
+        }
+    };
+#pragma unroll
+    for (int u = 0; u < R; ++u) issue(ar[u]);
+
+    f32x4_t acc[2][8];
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[g][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    int cst = 0;     // query stage of the position being consumed
+    int m = 0, kc = 0;
+    for (int f0 = 0; f0 < F; f0 += R) {
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+            if (f0 + u >= F) break;
+            // this position's query stage has landed (6 (R - 1) + 4 younger ops) in
+            // every wave, and every wave has read the stage the next DMA overwrites
+            asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"(6 * (R - 1) + 4) : "memory");
+            const char* Bs = smem + cst * HT;
+            cst = cst + 1 == NB ? 0 : cst + 1;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                uint4 fb[2];
+#pragma unroll
+                for (int hs = 0; hs < 2; ++hs)
+                    fb[hs] = *reinterpret_cast<const uint4*>(Bs + swz(j * 16 + r16, kq + 4 * hs));
+#pragma unroll
+                for (int hs = 0; hs < 2; ++hs)
+#pragma unroll
+                    for (int g = 0; g < 2; ++g) {
+                        if constexpr (std::is_same<T, f16_t>::value)
+                            acc[g][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                                __builtin_bit_cast(f16x8_t, ar[u][g][hs]), __builtin_bit_cast(f16x8_t, fb[hs]),
+                                acc[g][j], 0, 0, 0);
+                        else
+                            acc[g][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                                __builtin_bit_cast(bf16x8_t, ar[u][g][hs]), __builtin_bit_cast(bf16x8_t, fb[hs]),
+                                acc[g][j], 0, 0, 0);
+                    }
+            }
+            issue(ar[u]);  // position f + R into the ring slot just consumed
+            if (++kc == nk) {
+                // ---- tile epilogue: scores (database row c + r, query p)
+                const int c0 = (s_x + li + m * nb_x) * 256;
+                float* __restrict__ Y = (float*)a.y;
+#pragma unroll
+                for (int g = 0; g < 2; ++g) {
+                    const int c = c0 + 32 * wave + 16 * g + 4 * kq;
+                    if (c >= a.cout) continue;
+                    const bool full = c + 3 < a.cout;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const int p = j * 16 + r16;
+                        if (p >= a.P) continue;
+                        float v[4];
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) v[r] = acc[g][j][r];
+                        acc[g][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+                        if (a.scr_k) {
+                            screen_append(a, v, c, a.cout, p, a.scr_tau[p]);
+                            continue;
+                        }
+                        const long long o = (long long)p * a.ldy + c;
+                        if (full) {
+                            St4<float>::st(Y + o, v);
+                        } else {
+                            for (int r = 0; r < 4; ++r)
+                                if (c + r < a.cout) Y[o + r] = v[r];
+                        }
+                    }
+                }
+#pragma unroll
+                for (int g = 0; g < 2; ++g)
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) acc[g][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+                kc = 0;
+                ++m;
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing positions' operations
+}
+
+// ---------------------------------------------------------------------------
 // The mirror of k_gemm8h for 128-channel convs (auto: the strided mod3 3x3,
 // 699 vs 775 us on k_igemm at 128 images; the stride-1 mod3 3x3 stays on the
 // direct k_conv3x3, 550 vs 664 us on this kernel):
@@ -1419,7 +1581,15 @@ static bool try_gemm8(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
         // (25.69 / 25.73 vs 25.77 / 26.13 ms).  RR_TUNE_GEMM8 = 2 forces persistence
         // everywhere, | 4 forces one block per tile.
         const long long cus = grid_cus();
-        const bool persist = !g_gemm8_tile && (g_gemm8 == 2 || !std::is_same<T, TO>::value);
+        // Short-K 1x1 convs without a residual (<= 16 K-steps per tile) are persistent
+        // too: their epilogue reads BN scale / shift from LDS and its stores are counted
+        // into the next tile's first wait, so the next prologue lands under the epilogue
+        // (128 x R50 layers, same box: K = 512 540 -> 521 / 579 -> 552 us, K = 1024
+        // neutral to -8 us; K = 2048 and the 3x3s measured slower, so they stay one block
+        // per tile).
+        const bool short_k1 = k1 && a.kp / 64 <= 16 && !(a.flags & RR_CONV_RESIDUAL);
+        const bool persist = !g_gemm8_tile && (g_gemm8 == 2 || !std::is_same<T, TO>::value ||
+                                               (std::is_same<T, TO>::value && short_k1));
         // (a grid below 8 blocks would leave some XCD's tile range without a block)
         const dim3 g((unsigned)(!persist || cus < 8 || ntiles < cus ? ntiles : cus)), b(512);
 #define RR_G8(KMV, PV) hipLaunchKernelGGL((k_gemm8<T, TO, KMV, PV>), g, b, 0, s, a, tiles_p, (int)ntiles)
@@ -1438,6 +1608,7 @@ static bool try_gemm8(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
 }
 
 static int g_gemm8h = 1;  // rr_set_tuning(RR_TUNE_GEMM8, value | 8): k_gemm8h off
+static int g_gemm8s = 1;  // rr_set_tuning(RR_TUNE_GEMM8, value | 32): k_gemm8h instead of k_gemm8s
 
 // k_gemm8h: 16-bit 1x1 score GEMM (float out, natural row order, no affine /
 // residual / activation) with <= 128 "pixels" (queries), long channel dim.
@@ -1452,7 +1623,15 @@ static bool try_gemm8h(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
             return false;
         const long long ntiles = ((long long)a.cout + 255) / 256;
         if (ntiles >= (1ll << 31)) return false;
-        hipLaunchKernelGGL((k_gemm8h<T>), dim3((unsigned)ntiles), dim3(512), 0, s, a, (int)ntiles);
+        if (g_gemm8s) {
+            // persistent streaming form: one block per CU (a grid below 8 blocks
+            // would leave some XCD's tile range without a block)
+            const long long cus = grid_cus();
+            const unsigned g = (unsigned)(cus < 8 || ntiles < cus ? ntiles : cus);
+            hipLaunchKernelGGL((k_gemm8s<T, 6>), dim3(g), dim3(512), 0, s, a, (int)ntiles);
+        } else {
+            hipLaunchKernelGGL((k_gemm8h<T>), dim3((unsigned)ntiles), dim3(512), 0, s, a, (int)ntiles);
+        }
         return true;
     }
 }
@@ -1550,6 +1729,7 @@ void set_gemm_tuning(int key, int value) {
     else if (key == RR_TUNE_GEMM8) {
         g_gemm8h = !(value >= 0 && (value & 8));
         g_gemm8a = !(value >= 0 && (value & 16));
+        g_gemm8s = !(value >= 0 && (value & 32));
         g_gemm8_tile = value >= 0 && (value & 4);
         value = value < 0 ? 0 : value & 3;
         g_gemm8 = value > 2 ? 2 : value;

@@ -100,6 +100,14 @@ template <> struct DT<f16_t> {  // IEEE binary16, round to nearest even
     static __device__ __forceinline__ f16_t from_f(float v) { return (f16_t)v; }
 };
 
+// 16-B / 8-B global accesses of the streaming kernels (rr_stream.hip): data
+// read or written exactly once per launch.  (Marking them nontemporal -- nt
+// stores, nt loads and nt LDS-DMA -- measured 7 % slower on the body: 27.2-27.3
+// vs 25.4 ms per 128-image forward, same box; kept plain.)
+__device__ __forceinline__ void st16_once(void* p, uint4 v) { *reinterpret_cast<uint4*>(p) = v; }
+__device__ __forceinline__ void st8_once(void* p, uint2 v) { *reinterpret_cast<uint2*>(p) = v; }
+__device__ __forceinline__ uint4 ld16_once(const void* p) { return *reinterpret_cast<const uint4*>(p); }
+
 // Packed-k offset (elements) of K-step kt of a tap-uniform im2col conv (c_in a
 // multiple of the bk-deep K-step, k = tap * c_in + ci in the packed row), in
 // (input chunk, tap) order: every conv kernel of the engine -- the direct 3x3s

@@ -120,7 +120,7 @@ __global__ void __launch_bounds__(64 * NW) k_stream1x1(ConvArgs a, int nslices, 
             for (int j = 0; j < FN; ++j) {
                 const bf16_t* src = R + pix(s, j) * a.ldy + c0 + 8 * kq;
 #pragma unroll
-                for (int i2 = 0; i2 < NR; ++i2) dst[j][i2] = *reinterpret_cast<const uint4*>(src + 32 * i2);
+                for (int i2 = 0; i2 < NR; ++i2) dst[j][i2] = ld16_once(src + 32 * i2);  // residual: read once
             }
         }
     };
@@ -204,7 +204,7 @@ __global__ void __launch_bounds__(64 * NW) k_stream1x1(ConvArgs a, int nslices, 
                         o.y = H16<H>::pack2(v[2], v[3]);
                         o.z = H16<H>::pack2(v[4], v[5]);
                         o.w = H16<H>::pack2(v[6], v[7]);
-                        if (p < P) *reinterpret_cast<uint4*>(Y + p * a.ldy + c0 + cl) = o;
+                        if (p < P) st16_once(Y + p * a.ldy + c0 + cl, o);
                     }
                 }
             }
@@ -305,15 +305,15 @@ __global__ void __launch_bounds__(512) k_stream_pair(PairArgs a) {
         const long long p = pix(s);
         const bf16_t* xs = a.x + p * K3 + 8 * kq;
 #pragma unroll
-        for (int kk = 0; kk < NK3; ++kk) bq[d][kk] = *reinterpret_cast<const uint4*>(xs + kk * 32);
+        for (int kk = 0; kk < NK3; ++kk) bq[d][kk] = ld16_once(xs + kk * 32);
         if constexpr (PROJ) {
             const bf16_t* ps = a.xp + p * K3 + 8 * kq;
 #pragma unroll
-            for (int kk = 0; kk < NK3; ++kk) rq[d][kk] = *reinterpret_cast<const uint4*>(ps + kk * 32);
+            for (int kk = 0; kk < NK3; ++kk) rq[d][kk] = ld16_once(ps + kk * 32);
         } else {
             const bf16_t* rs = a.res + p * C3 + 8 * kq;
 #pragma unroll
-            for (int i2 = 0; i2 < NR3; ++i2) rq[d][i2] = *reinterpret_cast<const uint4*>(rs + 32 * i2);
+            for (int i2 = 0; i2 < NR3; ++i2) rq[d][i2] = ld16_once(rs + 32 * i2);
         }
     };
 #pragma unroll
@@ -377,7 +377,7 @@ __global__ void __launch_bounds__(512) k_stream_pair(PairArgs a) {
                 yq[i2].y = H16<H>::pack2(v[2], v[3]);
                 yq[i2].z = H16<H>::pack2(v[4], v[5]);
                 yq[i2].w = H16<H>::pack2(v[6], v[7]);
-                if (st) *reinterpret_cast<uint4*>(a.y + p * C3 + c) = yq[i2];
+                if (st) st16_once(a.y + p * C3 + c, yq[i2]);
             }
             load(d, strip_of(i + D));  // refill this slot: strip i + D
             // ---- z = act1(W1 y * s1 + h1), y straight from registers
@@ -412,7 +412,7 @@ __global__ void __launch_bounds__(512) k_stream_pair(PairArgs a) {
                 o.y = H16<H>::pack2(v[2], v[3]);
                 o.z = H16<H>::pack2(v[4], v[5]);
                 o.w = H16<H>::pack2(v[6], v[7]);
-                if (st) *reinterpret_cast<uint4*>(a.z + p * C1 + c) = o;
+                if (st) st16_once(a.z + p * C1 + c, o);
             }
         }
     }
@@ -604,7 +604,7 @@ __global__ void __launch_bounds__(512, 1) k_pair_mid(PairMidArgs a) {
                 o.w = H16<H>::pack2(v[6], v[7]);
                 *slot = o;
                 const long long p = (long long)t * TP + px;
-                if (p < P) *reinterpret_cast<uint4*>(a.y + p * C3 + c) = o;
+                if (p < P) st16_once(a.y + p * C3 + c, o);
             }
         }
         // y tile complete in LDS; x buffer free
@@ -642,7 +642,7 @@ __global__ void __launch_bounds__(512, 1) k_pair_mid(PairMidArgs a) {
                 o.x = H16<H>::pack2(v[0], v[1]);
                 o.y = H16<H>::pack2(v[2], v[3]);
                 const long long p = (long long)t * TP + 16 * j + r16;
-                if (p < P) *reinterpret_cast<uint2*>(a.z + p * C1 + c) = o;
+                if (p < P) st8_once(a.z + p * C1 + c, o);
             }
         }
     }

@@ -208,3 +208,23 @@ def test_process_decoder_ring_matches_thread_loader(tmp_path):
         assert not d.owns(big) and big.shape == (90, 120, 3)
     finally:
         d.close()
+
+
+def test_pinned_block_pool_free_list():
+    """extract_vectors' pinned block pool: a request takes the smallest free block
+    that holds it (by identity, never by tensor comparison), hands out a view of the
+    requested shape, and takes back only its own views once their event completes."""
+    from cirtorch.models.GF_net import _PinnedBlocks
+
+    class Done:
+        def query(self):
+            return True
+
+    pool = _PinnedBlocks()
+    pool.free = [torch.zeros(100, dtype=torch.uint8), torch.zeros(50, dtype=torch.uint8),
+                 torch.zeros(80, dtype=torch.uint8)]
+    v = pool.acquire((2, 20))
+    assert v.shape == (2, 20) and sorted(b.numel() for b in pool.free) == [80, 100]
+    pool.release([v, torch.zeros(3, dtype=torch.uint8)], Done())   # a foreign tensor is ignored
+    pool._reclaim()
+    assert sorted(b.numel() for b in pool.free) == [50, 80, 100]

@@ -56,6 +56,9 @@ d=json.loads(open('$OUT/benchenv_$i.json').read().strip().splitlines()[-1]); pri
         --output-format csv -- python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --no-extras --latency 0 --pcie-steps 0 --fp16-steps 0 \
         > "$OUT/prof_bench.json" 2> "$OUT/prof.err") || { tail -20 "$OUT/prof.err"; exit 1; }
       tail -c 1500 "$OUT/prof_bench.json" ;;
+    pmc)
+      timeout -k 10 900 bash "$ROOT/tools/pmc_round.sh" "gpurun_out/$TAG/pmc" > "$OUT/pmc.log" 2>&1 || { tail -20 "$OUT/pmc.log"; exit 1; }
+      tail -2 "$OUT/pmc.log" ;;
     *) echo "unknown step $STEP"; exit 2 ;;
   esac
 done
