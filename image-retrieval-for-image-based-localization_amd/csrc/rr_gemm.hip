@@ -641,6 +641,15 @@ __global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int n
             lds_sh[c] = a.shift[c];
         }
     }
+    // kNN screening (float out, natural order): the same region holds the queries'
+    // thresholds (<= 1024) and the 8 waves' survivor lists (ScreenStage)
+    uint32_t* const lds_tau = reinterpret_cast<uint32_t*>(smem + 8 * HT);
+    uint32_t* const lds_stage = lds_tau + 1024;
+    static_assert(4 * (1024 + 8 * 3 * ScreenStage::CAP) <= 2 * SS_MAX * 4, "screen staging fits the region");
+    const bool tau_lds = !PERM && sizeof(TO) == 4 && a.scr_k && a.P <= 1024;
+    if (tau_lds) {
+        for (int q = tid; q < a.P; q += 512) lds_tau[q] = a.scr_tau[q];
+    }
     const int wn = wave & 3;                // 32-column quarter of each quadrant
     // XCD-contiguous bijective tile order (blocks are dispatched round-robin over 8 XCDs)
     // Persistent blocks over an XCD-contiguous tile order: XCD x (blocks are
@@ -868,8 +877,34 @@ __global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int n
     // ---- epilogue: folded BN scale / shift, residual, activation, NHWC store
     if constexpr (PERM && sizeof(TO) == 2)
         prev_full = !resid && (ss_lds || !affine) && ec0 + 256 <= a.cout && ep0 + 256 <= a.P;
+    bool screened = false;
+    if constexpr (!PERM && sizeof(TO) == 4) {
+        if (a.scr_k) {  // kNN screen: stage the survivors, append them in batches, store nothing
+            screened = true;
+            ScreenStage st{lds_stage + wave * 3 * ScreenStage::CAP, 0};
 #pragma unroll
-    for (int qa = 0; qa < 2; ++qa) {
+            for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+                        for (int j = 0; j < 2; ++j) {
+                            const int c = ec0 + qa * 128 + grp * 64 + i * 16 + 4 * kq;
+                            const int p = ep0 + qb * 128 + wn * 32 + j * 16 + r16;
+                            const bool ok = p < a.P;
+                            uint32_t tau = 0xffffffffu;
+                            if (ok) tau = tau_lds ? lds_tau[p] : a.scr_tau[p];
+                            float v[4];
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) v[r] = acc[qa][qb][i][j][r] * 1.f + 0.f;  // (as the affine-free store path)
+                            st.add(a, v, c, a.cout, p, ok, tau);
+                        }
+            st.flush(a);
+        }
+    }
+#pragma unroll
+    for (int qa = 0; qa < 2 && !screened; ++qa) {
         if constexpr (PERM) {
 #pragma unroll
             for (int i2 = 0; i2 < 2; ++i2) {
@@ -1168,7 +1203,8 @@ template <typename T, int R>
 __global__ void __launch_bounds__(512, 1) k_gemm8s(ConvArgs a, int ntiles) {
     static_assert(sizeof(T) == 2 && 6 * (R - 1) + 4 <= 63, "16-bit operands, vmcnt range");
     constexpr int ESZ = 2, HT = 16384, NB = R + 1;
-    __shared__ __attribute__((aligned(1024))) char smem[NB * HT];
+    // query stages + the queries' thresholds (<= 128) + 8 survivor lists (ScreenStage)
+    __shared__ __attribute__((aligned(1024))) char smem[NB * HT + 4 * (128 + 8 * 3 * ScreenStage::CAP)];
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1192,6 +1228,11 @@ __global__ void __launch_bounds__(512, 1) k_gemm8s(ConvArgs a, int ntiles) {
     for (int i = 0; i < 2; ++i) {
         const int p = (wave + 8 * i) * 8 + lrow;
         b_off[i] = p < a.P ? (unsigned)(((long long)p * a.cin + lchunk * 8) * ESZ) : OOB;
+    }
+    uint32_t* const lds_tau = reinterpret_cast<uint32_t*>(smem + NB * HT);
+    uint32_t* const lds_stage = lds_tau + 128;
+    if (a.scr_k) {
+        for (int q = tid; q < a.P; q += 512) lds_tau[q] = a.scr_tau[q];
     }
     // issue side: stream position (mi, ki); this lane's two DB rows of tile mi
     // (positions past the block's stream re-read its last tile: same count of
@@ -1271,8 +1312,23 @@ __global__ void __launch_bounds__(512, 1) k_gemm8s(ConvArgs a, int ntiles) {
                 // ---- tile epilogue: scores (database row c + r, query p)
                 const int c0 = (s_x + li + m * nb_x) * 256;
                 float* __restrict__ Y = (float*)a.y;
+                if (a.scr_k) {  // stage the survivors, append them in batches (full-wave control flow)
+                    ScreenStage st{lds_stage + wave * 3 * ScreenStage::CAP, 0};
 #pragma unroll
-                for (int g = 0; g < 2; ++g) {
+                    for (int g = 0; g < 2; ++g)
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) {
+                            const int p = j * 16 + r16;
+                            const bool ok = p < a.P;
+                            float v[4];
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) v[r] = acc[g][j][r];
+                            st.add(a, v, c0 + 32 * wave + 16 * g + 4 * kq, a.cout, p, ok, ok ? lds_tau[p] : 0xffffffffu);
+                        }
+                    st.flush(a);
+                }
+#pragma unroll
+                for (int g = 0; g < 2 && !a.scr_k; ++g) {
                     const int c = c0 + 32 * wave + 16 * g + 4 * kq;
                     if (c >= a.cout) continue;
                     const bool full = c + 3 < a.cout;

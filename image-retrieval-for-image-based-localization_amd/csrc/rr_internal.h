@@ -179,6 +179,56 @@ __device__ __forceinline__ void screen_append(const ConvArgs& a, const float* v,
         }
     }
 }
+// Staged screening epilogue (k_gemm8 / k_gemm8s): the survivors of a wave are
+// first compacted into a wave-private LDS list (ballot + mbcnt: no atomics, no
+// waits), and appended to their (query, chunk) slots in batches of 64, one
+// lane per survivor, so a wave waits for one round of atomic returns per 64
+// survivors instead of one per fragment that holds a survivor.  Which KC of an
+// overflowing slot's survivors are stored does not matter: k_slot_fixup
+// rebuilds every slot whose count exceeds KC, and a slot's candidates are a set
+// (the final select orders them by key, then row).  Every lane of the wave must
+// call add() / flush() (full-wave control flow): validity goes in `ok`.
+struct ScreenStage {
+    static constexpr int CAP = 128;  // entries per wave: key, global row, query (3 words each)
+    uint32_t* e;                     // this wave's LDS list
+    int n;                           // staged entries (wave-uniform)
+    __device__ __forceinline__ void flush(const ConvArgs& a) {
+        const int lane = threadIdx.x & 63;
+        for (int b = 0; b < n; b += 64) {
+            const int k = b + lane;
+            if (k < n) {
+                const uint32_t key = e[3 * k], grow = e[3 * k + 1], p = e[3 * k + 2];
+                const long long slot = (long long)p * a.scr_nchunks + (int)grow / a.scr_L;
+                const int pos = atomicAdd(a.scr_cnt + slot, 1);
+                if (pos < a.scr_KC) {
+                    a.scr_k[slot * a.scr_KC + pos] = key;
+                    a.scr_i[slot * a.scr_KC + pos] = (int)grow;
+                }
+            }
+        }
+        n = 0;
+    }
+    // scores v[0..3] of database rows c..c+3 (valid: < rows) and query p (valid: ok)
+    __device__ __forceinline__ void add(const ConvArgs& a, const float* v, int c, int rows, int p, bool ok,
+                                        uint32_t tau) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t key = score_key(v[r]);
+            const bool s = ok && c + r < rows && key >= tau;
+            const unsigned long long m = __ballot(s);
+            if (m == 0ull) continue;  // wave-uniform
+            if (n + 64 > CAP) flush(a);
+            if (s) {
+                const int k = n + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+                e[3 * k] = key;
+                e[3 * k + 1] = (uint32_t)(a.scr_row0 + c + r);
+                e[3 * k + 2] = (uint32_t)p;
+            }
+            n += __popcll(m);
+        }
+    }
+};
 // scores[p][c] (f32, row stride ldy) = x[p][:] . w[c][:], 1x1 GEMM, dtype in.
 void gemm_scores(const ConvArgs& a, int dtype, hipStream_t s);
 
