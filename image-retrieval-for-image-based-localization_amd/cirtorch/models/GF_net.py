@@ -430,14 +430,23 @@ def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], 
         procs = decode_procs.get(workers, 2 * ahead + 2 * batch + 8)
 
     class _ProcFuture:
-        def __init__(self, i):
-            self.p = procs.submit(images[i], image_size, bbxs[i] if bbxs is not None else None)
+        def __init__(self, p):
+            self.p = p
 
         def result(self):
             return "hwc", self.p.result()
 
-    def submit(pool, i):
-        return _ProcFuture(i) if procs is not None else pool.submit(decode, i)
+    def submit_next(pool, futs, nxt):
+        """submit input nxt (files through the process decoder: up to 4 per task) -> next index"""
+        if procs is None:
+            futs.append((nxt, pool.submit(decode, nxt)))
+            return nxt + 1
+        hi = min(n, nxt + 4)
+        ps = procs.submit_group([(images[i], image_size, bbxs[i] if bbxs is not None else None)
+                                 for i in range(nxt, hi)])
+        for i, p in zip(range(nxt, hi), ps):
+            futs.append((i, _ProcFuture(p)))
+        return hi
 
     try:
         with ThreadPoolExecutor(max_workers=max(1, workers)) as pool, torch.no_grad():
@@ -454,14 +463,12 @@ def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], 
                 run([i for i, _ in g], [x for _, x in g], hwc=key[0] == "hwc")
 
             while nxt < n and len(futs) < ahead:
-                futs.append((nxt, submit(pool, nxt)))
-                nxt += 1
+                nxt = submit_next(pool, futs, nxt)
             while futs:
                 i, f = futs.popleft()
                 kind, x = f.result()
-                if nxt < n:
-                    futs.append((nxt, submit(pool, nxt)))
-                    nxt += 1
+                if nxt < n and len(futs) < ahead:
+                    nxt = submit_next(pool, futs, nxt)
                 key = (kind, tuple(x.shape), x.dtype, x.is_cuda)
                 groups.setdefault(key, []).append((i, x))
                 buffered += 1

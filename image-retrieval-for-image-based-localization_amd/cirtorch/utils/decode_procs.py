@@ -52,13 +52,20 @@ def _decode_into(args):
     return a.shape, None
 
 
+def _decode_group(group):
+    """several files per task: one IPC round trip (pickling in the parent holds
+    its GIL) per group instead of per image"""
+    return [_decode_into(g) for g in group]
+
+
 class _Pending:
-    def __init__(self, owner, slot, res):
-        self.owner, self.slot, self.res = owner, slot, res
+    def __init__(self, owner, slot, res, k=None):
+        self.owner, self.slot, self.res, self.k = owner, slot, res, k
 
     def result(self):
         import torch
-        shape, big = self.res.get(timeout=300)
+        out = self.res.get(timeout=300)
+        shape, big = out if self.k is None else out[self.k]
         if big is not None:
             self.owner._give_back([self.slot])
             return torch.from_numpy(big)
@@ -130,6 +137,22 @@ class ProcDecoder:
             slot = self.free.pop()
         res = self.pool.apply_async(_decode_into, ((path, imsize, bbx, slot * self.slot_bytes, self.slot_bytes),))
         return _Pending(self, slot, res)
+
+    def submit_group(self, items):
+        """items: [(path, imsize, bbx)] -> one pending image each, decoded by one task"""
+        slots = []
+        with self.lock:
+            for _ in items:
+                self._reclaim(block=False)
+                if not self.free:
+                    self._reclaim(block=True)
+                if not self.free:
+                    self.free.extend(slots)
+                    raise RuntimeError("ProcDecoder: every slot is held by an undelivered image (ring too small)")
+                slots.append(self.free.pop())
+        res = self.pool.apply_async(_decode_group, ([(p, s_, b, sl * self.slot_bytes, self.slot_bytes)
+                                                     for (p, s_, b), sl in zip(items, slots)],))
+        return [_Pending(self, sl, res, k) for k, sl in enumerate(slots)]
 
     def owns(self, t):
         return t.data_ptr() in self.slot_of

@@ -727,8 +727,12 @@ int rr_knn_topk_checked(const void* db, const float* db_f32, long long n_db, con
     // select launch); overflowing slots are rebuilt by k_slot_fixup.
     // RR_KNN_FUSED=0: every chunk through the slab (the round-1 pipeline).
     static const int fused_env = getenv("RR_KNN_FUSED") && getenv("RR_KNN_FUSED")[0] == '0' ? 0 : 1;
-    const bool fused = fused_env && g_knn_fused && p.nchunks > PREFIX_CHUNKS && (d * esz) % 128 == 0;
-    const int g0 = fused ? PREFIX_CHUNKS : p.nchunks;
+    // RR_KNN_PREFIX: prefix chunks (A/B knob; any count gives the same results -- tau is
+    // a valid bound whatever the prefix, and overflowing slots are rebuilt)
+    static const int prefix = getenv("RR_KNN_PREFIX") ? atoi(getenv("RR_KNN_PREFIX")) : PREFIX_CHUNKS;
+    const int pre = prefix >= 1 ? prefix : PREFIX_CHUNKS;
+    const bool fused = fused_env && g_knn_fused && p.nchunks > pre && (d * esz) % 128 == 0;
+    const int g0 = fused ? pre : p.nchunks;
     const long long slab_rows = (long long)g0 * p.L < n_db ? (long long)g0 * p.L : n_db;
     // the running threshold is reset by a kernel (RR_KNN_TAU_MEMSET=1: by
     // hipMemsetAsync, kept to reproduce the graph-replay finding of DESIGN §4)

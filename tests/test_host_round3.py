@@ -206,6 +206,10 @@ def test_process_decoder_ring_matches_thread_loader(tmp_path):
             d.release(outs, Done())
         big = d.submit(paths[2], None, None).result()      # 90 x 120 x 3 > one slot
         assert not d.owns(big) and big.shape == (90, 120, 3)
+        # several files per task (extract_vectors submits groups of 4)
+        outs = [q.result() for q in d.submit_group([(p, None, None) for p in (paths[0], paths[1], paths[3])])]
+        for p, t in zip((paths[0], paths[1], paths[3]), outs):
+            assert (t.numpy() == np.asarray(_load_pil(p, None, None), dtype=np.uint8)).all(), p
     finally:
         d.close()
 
