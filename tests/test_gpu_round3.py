@@ -178,6 +178,34 @@ def test_extract_vectors_device_tensors(cuda):
 
 
 
+def test_extract_vectors_process_decoder_equals_threads_and_batch1(cuda, tmp_path, monkeypatch):
+    """A file list long enough for the process decoder (>= 2 x batch: spawned
+    workers, page-locked shared-memory ring, grouped tasks, early short chains)
+    gives the same bits as decode threads and as one image at a time; mixed sizes,
+    bbx crops, JPEG and PNG."""
+    import numpy as np
+    from PIL import Image
+    from cirtorch.models.GF_net import extract_vectors, make_net
+    from cirtorch.models.init import random_init_
+    net = random_init_(make_net("resnet18", precision="bf16"), 6).to(cuda).eval()
+    r = np.random.default_rng(8)
+    paths, bbxs = [], []
+    for i in range(22):
+        h, w = [(96, 128), (128, 96), (80, 112)][i % 3]
+        a = (r.random((h, w, 3)) * 255).astype(np.uint8)
+        p = str(tmp_path / ("f%02d.%s" % (i, "jpg" if i % 2 else "png")))
+        Image.fromarray(a).save(p)
+        paths.append(p)
+        bbxs.append((3, 5, w - 7, h - 2) if i % 5 == 0 else None)
+    procs = extract_vectors(net, paths, None, bbxs=bbxs, batch=4)
+    monkeypatch.setenv("RR_DECODE_PROCS", "0")
+    threads = extract_vectors(net, paths, None, bbxs=bbxs, batch=4)
+    assert torch.equal(procs, threads)
+    for i in (0, 7, 21):
+        one = extract_vectors(net, [paths[i]], None, bbxs=[bbxs[i]], batch=4)
+        assert torch.equal(procs[:, i:i + 1], one), i
+
+
 def _unit_rows(n, d, seed, dup_every=0):
     g = torch.Generator().manual_seed(seed)
     x = torch.randn(n, d, generator=g)
