@@ -409,7 +409,9 @@ def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], 
     # images (partial groups: when the buffered images exceed `ahead`, the
     # largest one runs; the rest at the end), so extraction overlaps decoding.
     ahead = max(2, 4 * batch)
-    min_chain = max(1, min(batch, 16))
+    # shortest chain started early while the GPU idles (RR_EV_MIN_CHAIN: A/B knob; 16 / 32 / 64
+    # within the host's noise on 128 JPEGs, profiles/r03_ab/r03q_dropin_sched_ab.txt)
+    min_chain = max(1, min(batch, int(os.environ.get("RR_EV_MIN_CHAIN", "32"))))
     pinned_files = transform is None and test_transform is None
 
     def decode(i):
@@ -429,6 +431,8 @@ def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], 
         # + the chains whose H2D copy is in flight (<= 2 x batch)
         procs = decode_procs.get(workers, 2 * ahead + 2 * batch + 8)
 
+    first1 = workers if os.environ.get("RR_EV_FIRST1", "0") == "1" else 0  # single-file first tasks (A/B knob)
+
     class _ProcFuture:
         def __init__(self, p):
             self.p = p
@@ -437,11 +441,12 @@ def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], 
             return "hwc", self.p.result()
 
     def submit_next(pool, futs, nxt):
-        """submit input nxt (files through the process decoder: up to 4 per task) -> next index"""
+        """submit input nxt (files through the process decoder: up to 4 per task, one
+        per task for the first `workers` files so the first chain starts early) -> next index"""
         if procs is None:
             futs.append((nxt, pool.submit(decode, nxt)))
             return nxt + 1
-        hi = min(n, nxt + 4)
+        hi = min(n, nxt + (1 if nxt < first1 else 4))
         ps = procs.submit_group([(images[i], image_size, bbxs[i] if bbxs is not None else None)
                                  for i in range(nxt, hi)])
         for i, p in zip(range(nxt, hi), ps):

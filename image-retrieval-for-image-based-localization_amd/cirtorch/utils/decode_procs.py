@@ -32,10 +32,14 @@ def _worker_init(name):
 
 
 def _load(path, imsize, bbx):
-    """GF_net._load_pil, restated for a process that does not import torch"""
+    """GF_net._load_pil, restated for a process that does not import torch (an RGB
+    file skips convert("RGB"), which would only copy it: same pixels)"""
     from PIL import Image
     with open(path, "rb") as f:
-        img = Image.open(f).convert("RGB")
+        img = Image.open(f)
+        img.load()
+    if img.mode != "RGB":
+        img = img.convert("RGB")
     if bbx is not None:
         img = img.crop(bbx)
     if imsize is not None:
@@ -45,11 +49,13 @@ def _load(path, imsize, bbx):
 
 def _decode_into(args):
     path, imsize, bbx, off, cap = args
-    a = np.asarray(_load(path, imsize, bbx), dtype=np.uint8)
-    if a.nbytes > cap:
-        return a.shape, a
-    np.copyto(np.ndarray(a.shape, np.uint8, buffer=_SHM.buf, offset=off), a)
-    return a.shape, None
+    img = _load(path, imsize, bbx)
+    data = img.tobytes()  # raw RGB rows: one copy, then one into the ring
+    shape = (img.height, img.width, 3)
+    if len(data) > cap:
+        return shape, np.frombuffer(data, np.uint8).reshape(shape).copy()
+    _SHM.buf[off:off + len(data)] = data
+    return shape, None
 
 
 def _decode_group(group):
