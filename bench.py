@@ -63,7 +63,9 @@ def parse():
     ap.add_argument("--no-overlap", dest="overlap", action="store_false",
                     help="run each step's match on the extraction stream (default: on a second stream, overlapping "
                          "the next step's extraction; +0.8-1.5 %% on one GPU, DESIGN.md)")
-    ap.add_argument("--cpu-images", type=int, default=2)
+    ap.add_argument("--cpu-images", type=int, default=12,
+                    help="images of the CPU baseline's extract sample (batch 1, as scripts/test.py)")
+    ap.add_argument("--cpu-queries", type=int, default=32, help="queries of the CPU baseline's match sample")
     ap.add_argument("--cpu-db-rows", type=int, default=1_000_000,
                     help="rows of the CPU baseline's match sample (1M = the full headline DB, no extrapolation)")
     ap.add_argument("--no-extras", dest="extras", action="store_false",
@@ -160,7 +162,7 @@ def cpu_baseline(args):
             net.forward_padded(imgs[i:i + 1])     # reference test batch size is 1 (base.ini:143)
         t_ext = (time.perf_counter() - t0) / args.cpu_images
     db = data.database(args.cpu_db_rows, args.dim)
-    q = data.queries(8, args.dim)
+    q = data.queries(args.cpu_queries, args.dim)
     t0 = time.perf_counter()
     scores = np.dot(db, q.T)                      # scripts/test.py:247
     ranks = np.argsort(-scores, axis=0)           # scripts/test.py:248
@@ -174,10 +176,10 @@ def cpu_baseline(args):
             "host_cpu": model, "sockets": sockets, "logical_cpus": os.cpu_count(),
             "extract_s_per_image": t_ext, "match_s_per_query": t_match,
             "sample": ("oracle restatement (torch-CPU conv/BN/leaky + GeM/L2N/whiten) of %d x 3x%dx%d images "
-                       "at batch 1 (%.3f s/img) + the reference match np.dot + np.argsort(-scores, axis=0) of 8 "
+                       "at batch 1 (%.3f s/img) + the reference match np.dot + np.argsort(-scores, axis=0) of %d "
                        "queries against a %d x %d float32 DB%s (%.3f s/query); host %s, %d socket(s), %d threads used"
-                       % (args.cpu_images, args.height, args.width, t_ext, args.cpu_db_rows, args.dim, scaled, t_match,
-                          model, sockets, threads))}
+                       % (args.cpu_images, args.height, args.width, t_ext, args.cpu_queries, args.cpu_db_rows, args.dim,
+                          scaled, t_match, model, sockets, threads))}
 
 
 def host_cpu():
