@@ -63,6 +63,9 @@ def parse():
     ap.add_argument("--no-overlap", dest="overlap", action="store_false",
                     help="run each step's match on the extraction stream (default: on a second stream, overlapping "
                          "the next step's extraction; +0.8-1.5 %% on one GPU, DESIGN.md)")
+    ap.add_argument("--search-cus", type=int, default=0,
+                    help="cap the CUs the step's persistent search kernels spread over (RR_TUNE_GRID_CUS set "
+                         "around the search launches only), leaving the rest to the overlapped extraction; 0 = all")
     ap.add_argument("--cpu-images", type=int, default=12,
                     help="images of the CPU baseline's extract sample (batch 1, as scripts/test.py)")
     ap.add_argument("--cpu-queries", type=int, default=32, help="queries of the CPU baseline's match sample")
@@ -581,7 +584,15 @@ def main():
         q = desc.t().contiguous()
         if world > 1:
             q = all_gather_stacked(q).reshape(world * B, q.shape[1])
-        return state["index"].search(q, args.k)
+        if args.search_cus <= 0:
+            return state["index"].search(q, args.k)
+        # the cap is read when a kernel is launched: only the search's launches see it
+        from cirtorch import _engine as E
+        E.check(E.lib().rr_set_tuning(7, args.search_cus), "rr_set_tuning")
+        try:
+            return state["index"].search(q, args.k)
+        finally:
+            E.lib().rr_set_tuning(7, 0)
 
     EB = max(1, min(args.extract_batch, B))
 

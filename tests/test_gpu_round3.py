@@ -263,3 +263,23 @@ def test_batch_invariant_descriptors(cuda, precision):
     finally:
         E.lib().rr_set_tuning(7, 0)
     assert torch.equal(many[:, 3:4], one)
+
+
+@pytest.mark.parametrize("nq", [77, 300])
+@pytest.mark.parametrize("cap", [9, 64])
+def test_search_with_capped_grid_equals_full_grid(cuda, nq, cap):
+    """The persistent score GEMMs (k_gemm8s at <= 128 queries, k_gemm8 above) on a
+    capped grid (RR_TUNE_GRID_CUS, as bench.py --search-cus sets around the step's
+    search) give the same ranks and scores as on the whole chip."""
+    from cirtorch import _engine as E
+    from cirtorch.search import KnnIndex
+    db = _unit_rows(200_000, 2048, seed=31).to(cuda)
+    q = _unit_rows(nq, 2048, seed=32).to(cuda)
+    idx = KnnIndex(db, "bf16")
+    s0, i0 = idx.search(q, 50)
+    E.check(E.lib().rr_set_tuning(7, cap), "rr_set_tuning")
+    try:
+        s1, i1 = idx.search(q, 50)
+    finally:
+        E.lib().rr_set_tuning(7, 0)
+    assert torch.equal(i0, i1) and torch.equal(s0, s1)
