@@ -377,17 +377,74 @@ __device__ void bitonic_best_first(double* ks, I* is, int n) {
 //  k_final_select  grid (nq):          top KC of the chunk candidates -> sel_i[q][KC]
 //  k_rescore       grid (npow2/4, nq): one wave per candidate, float64 score
 //  k_final_sort    grid (nq):          bitonic (score desc, index asc), emit k
+// Staged form (`stage` true: nchunks <= FSEL_MAXCH, dynamic LDS of
+// FSEL_LDS bytes): the occupied slots' keys are gathered once, in slot order,
+// into LDS (one pass of independent loads) and the select's 5-8 passes read
+// LDS instead of re-walking the nchunks x KC slot array in L2.  Unoccupied
+// slots are (key 0, index -1) in the unstaged form; one such entry is appended
+// when any exists, so the K-th key (and thereby sel_thr) and the selected set
+// are the same.  Indices are read from the slot array for the taken keys only.
+constexpr int FSEL_CAP = 12288;   // staged keys (48 KiB): ~4.2k occupied for 1M rows at k = 100
+constexpr int FSEL_MAXCH = 1024;  // chunk offsets (4 KiB)
+constexpr size_t FSEL_LDS = (size_t)(FSEL_CAP + FSEL_MAXCH + 1) * 4;
 __global__ void __launch_bounds__(SEL_THREADS) k_final_select(const uint32_t* __restrict__ cand_k,
                                                               const int* __restrict__ cand_i,
                                                               const int* __restrict__ cnt, int nchunks, int KC,
                                                               uint32_t* __restrict__ sel_k, int* __restrict__ sel_i,
-                                                              uint32_t* __restrict__ sel_thr) {
+                                                              uint32_t* __restrict__ sel_thr, int stage) {
     __shared__ int smi[TOPK_BINS + 64];
+    extern __shared__ __attribute__((aligned(16))) char dyn[];
     const int q = blockIdx.x;
     const int ncand = nchunks * KC;
     const uint32_t* ck = cand_k + (long long)q * ncand;
     const int* ci = cand_i + (long long)q * ncand;
     const int* cq = cnt + (long long)q * nchunks;
+    if (stage) {
+        uint32_t* lk = reinterpret_cast<uint32_t*>(dyn);
+        int* off = reinterpret_cast<int*>(lk + FSEL_CAP);  // nchunks + 1 exclusive offsets
+        const int tid = threadIdx.x, lane = tid & 63;
+        if (tid < 64) {
+            int run = 0;
+            for (int b = 0; b < nchunks; b += 64) {
+                const int c = b + lane;
+                const int v = c < nchunks ? min(cq[c], KC) : 0;
+                int x = v;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int y = __shfl_up(x, o, 64);
+                    if (lane >= o) x += y;
+                }
+                if (c < nchunks) off[c] = run + x - v;
+                run += __shfl(x, 63, 64);
+            }
+            if (lane == 0) off[nchunks] = run;
+        }
+        __syncthreads();
+        const int total = off[nchunks];
+        if (total < FSEL_CAP) {  // block-uniform
+            for (int c = tid >> 6; c < nchunks; c += SEL_WAVES) {
+                const int o = off[c], v = off[c + 1] - o;
+                for (int j = lane; j < v; j += 64) lk[o + j] = ck[(long long)c * KC + j];
+            }
+            const bool pad = total < ncand;
+            if (pad && tid == 0) lk[total] = 0u;
+            __syncthreads();
+            auto gi = [&](int i) -> int {
+                if (i >= total) return -1;
+                int lo = 0, hi = nchunks;  // off[lo] <= i < off[hi]
+                while (hi - lo > 1) {
+                    const int mid = (lo + hi) >> 1;
+                    if (off[mid] <= i) lo = mid;
+                    else hi = mid;
+                }
+                return ci[(long long)lo * KC + (i - off[lo])];
+            };
+            const uint32_t thr = block_topk<false, true>([&](int i) { return lk[i]; }, gi, total + (pad ? 1 : 0), KC,
+                                                         sel_k + (long long)q * KC, sel_i + (long long)q * KC, smi);
+            if (threadIdx.x == 0) sel_thr[q] = thr;
+            return;
+        }
+    }
     // slot (chunk c, position j) holds a candidate when j < min(cnt, KC); the
     // chunk selects fill whole slots (sentinels (0, -1) past their survivors),
     // the screening epilogue appends in arbitrary order -> ties by index
@@ -780,8 +837,11 @@ int rr_knn_topk_checked(const void* db, const float* db_f32, long long n_db, con
     }
     const size_t fin_lds = (size_t)p.npow2 * 12;
     if (fin_lds > 160 * 1024 - 4096) return fail(RR_EINVAL, "rr_knn_topk: candidate set exceeds LDS");
-    hipLaunchKernelGGL(k_final_select, dim3(nq), dim3(SEL_THREADS), 0, s, cand_k, cand_i, cnt, p.nchunks, p.KC,
-                       sel_k, sel_i, sel_thr);
+    // RR_KNN_FSEL=0: the unstaged final select (A/B)
+    static const int fsel = getenv("RR_KNN_FSEL") ? atoi(getenv("RR_KNN_FSEL")) : 1;
+    const int stage = fsel && p.nchunks <= FSEL_MAXCH;
+    hipLaunchKernelGGL(k_final_select, dim3(nq), dim3(SEL_THREADS), stage ? FSEL_LDS : 0, s, cand_k, cand_i, cnt,
+                       p.nchunks, p.KC, sel_k, sel_i, sel_thr, stage);
     hipLaunchKernelGGL(k_rescore, dim3((p.npow2 + 3) / 4, nq), dim3(256), 0, s, sel_i, p.KC, p.npow2, db_f32, q_f32, d,
                        fin_s, fin_i);
     // screening error bound per unit ||q|| ||x||: input rounding of both
