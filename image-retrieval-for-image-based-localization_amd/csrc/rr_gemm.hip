@@ -1684,7 +1684,15 @@ static bool try_gemm8h(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
             // would leave some XCD's tile range without a block)
             const long long cus = grid_cus();
             const unsigned g = (unsigned)(cus < 8 || ntiles < cus ? ntiles : cus);
-            hipLaunchKernelGGL((k_gemm8s<T, 6>), dim3(g), dim3(512), 0, s, a, (int)ntiles);
+            // K-steps in flight per wave: 4 (Q = 128 vs 1M rows: 1.13 / 1.12 ms vs 1.15 / 1.14 at 6,
+            // 1.28 at 8, profiles/r03_ab/r03ac_gemm8s_depth_ab.txt); RR_GEMM8S_R = 3 or 6: A/B
+            static const int rdepth = getenv("RR_GEMM8S_R") ? atoi(getenv("RR_GEMM8S_R")) : 4;
+            if (rdepth == 6)
+                hipLaunchKernelGGL((k_gemm8s<T, 6>), dim3(g), dim3(512), 0, s, a, (int)ntiles);
+            else if (rdepth == 3)
+                hipLaunchKernelGGL((k_gemm8s<T, 3>), dim3(g), dim3(512), 0, s, a, (int)ntiles);
+            else
+                hipLaunchKernelGGL((k_gemm8s<T, 4>), dim3(g), dim3(512), 0, s, a, (int)ntiles);
         } else {
             hipLaunchKernelGGL((k_gemm8h<T>), dim3((unsigned)ntiles), dim3(512), 0, s, a, (int)ntiles);
         }
