@@ -47,6 +47,11 @@ _SIGS = {
                            _i, _i, _i, _vp], _i),
     "rr_stem_conv_pool_u8": ([_vp, _i, _i, _i, ctypes.POINTER(_f), ctypes.POINTER(_f), _i, _vp, _vp, _vp, _i, _f,
                               _vp, _i, _i, _i, _vp], _i),
+    "rr_image_to_nhwc_ragged": ([_vp, _vp, _i, _i, _i, _i, _i, ctypes.POINTER(_f), ctypes.POINTER(_f), _i, _vp, _i,
+                                 _i, _vp], _i),
+    "rr_stem_conv_pool_ragged": ([_vp, _vp, _i, _i, _i, _i, ctypes.POINTER(_f), ctypes.POINTER(_f), _i, _vp, _vp, _vp,
+                                  _i, _f, _vp, _i, _i, _i, _vp], _i),
+    "rr_pad_images": ([_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp], _i),
     "rr_maxpool2d": ([_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _i, _vp], _i),
     "rr_resize_bilinear": ([_vp, _i, _i, _i, _vp, _i, _i, _d, _d, _vp], _i),
     "rr_global_pool": ([_vp, _i, _i, _i, _i, _i, _f, _f, _vp, _i, _vp], _i),

@@ -170,6 +170,98 @@ def stem_conv_pool(img, wpk, scale, shift, leaky=True, slope=0.01, mean=None, st
     return y
 
 
+def _ragged(images):
+    """a ragged batch (list of [C, h_i, w_i] GPU tensors of one dtype, None entries
+    allowed) -> the C ABI's host (pointer, extent) arrays + the contiguous tensors
+    they point into (kept referenced until the launch is enqueued)."""
+    n = len(images)
+    ptrs = (ctypes.c_void_p * n)()
+    ext = (ctypes.c_int * (2 * n))()
+    kept = []
+    for i, t in enumerate(images):
+        if t is None:
+            continue
+        E.require_gpu(t)
+        t = t.contiguous()
+        kept.append(t)
+        ptrs[i] = t.data_ptr()
+        ext[2 * i], ext[2 * i + 1] = int(t.shape[-2]), int(t.shape[-1])
+    return ptrs, ext, kept
+
+
+def _norm_arrays(mean, std, c):
+    do = mean is not None
+    m = (ctypes.c_float * 4)(*(list(mean) + [0.0] * (4 - c))[:4]) if do else (ctypes.c_float * 4)()
+    s = (ctypes.c_float * 4)(*(list(std) + [1.0] * (4 - c))[:4]) if do else (ctypes.c_float * 4)(1, 1, 1, 1)
+    return m, s, int(do)
+
+
+def image_to_nhwc_ragged(images, h, w, c_pad, dtype, mean=None, std=None):
+    """ragged batch of [C, h_i, w_i] float32 or uint8 images (h_i <= h, w_i <= w) ->
+    [N, h, w, c_pad] `dtype`: the padded, normalised map (map pixels outside an
+    image read 0 before normalisation, utils/sequence.py:51 then utils/image.py:125)
+    without a padded copy of the inputs."""
+    ref = next(t for t in images if t is not None)
+    c = int(ref.shape[0])
+    u8 = ref.dtype == torch.uint8
+    if not u8 and ref.dtype != torch.float32:
+        images = [t.float() if t is not None else None for t in images]
+    ptrs, ext, kept = _ragged(images)
+    out = torch.empty((len(images), h, w, c_pad), dtype=dtype, device=ref.device)
+    m, s, do = _norm_arrays(mean, std, c)
+    E.check(E.lib().rr_image_to_nhwc_ragged(ptrs, ext, len(images), c, h, w, int(u8), m, s, do, E.ptr(out), c_pad,
+                                            E.dtype_code(dtype), _st()), "rr_image_to_nhwc_ragged")
+    return out
+
+
+def stem_conv_pool_ragged(images, h, w, wpk, scale, shift, leaky=True, slope=0.01, mean=None, std=None):
+    """The fused stem (stem_conv_pool) on a ragged batch padded to h x w: equals
+    stem_conv_pool on the padded batch bit for bit, with no padded copy."""
+    E.require_gpu(wpk, scale, shift)
+    ref = next(t for t in images if t is not None)
+    if ref.shape[0] != 3:
+        raise RuntimeError("stem_conv_pool: expected 3-channel images, got %d" % ref.shape[0])
+    u8 = ref.dtype == torch.uint8
+    if not u8 and ref.dtype != torch.float32:
+        images = [t.float() if t is not None else None for t in images]
+    ptrs, ext, kept = _ragged(images)
+    ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    hp, wp = (ho - 1) // 2 + 1, (wo - 1) // 2 + 1
+    y = torch.empty((len(images), hp, wp, 64), dtype=wpk.dtype, device=ref.device)
+    do = mean is not None
+    m = (ctypes.c_float * 3)(*mean) if do else (ctypes.c_float * 3)()
+    s = (ctypes.c_float * 3)(*std) if do else (ctypes.c_float * 3)(1, 1, 1)
+    E.check(E.lib().rr_stem_conv_pool_ragged(ptrs, ext, len(images), h, w, int(u8), m, s, int(do), E.ptr(wpk),
+                                             E.ptr(scale), E.ptr(shift), E.RR_ACT_LEAKY if leaky else E.RR_ACT_IDENTITY,
+                                             float(slope), E.ptr(y), hp, wp, E.dtype_code(wpk.dtype), _st()),
+            "rr_stem_conv_pool_ragged")
+    return y
+
+
+_ELEM_CT = {1: ctypes.c_uint8, 2: ctypes.c_uint16, 4: ctypes.c_uint32, 8: ctypes.c_uint64}
+
+
+def pad_images(images, h, w, pad_value=0.0):
+    """ragged batch of [C, h_i, w_i] (or [h_i, w_i]) GPU tensors -> one padded
+    [N, C, h, w] (or [N, h, w]) tensor, images top-left, pad_value elsewhere:
+    one rr_pad_images launch (utils/sequence.py:4-67)."""
+    ref = next(t for t in images if t is not None)
+    chw = ref.dim() == 3
+    c = int(ref.shape[0]) if chw else 1
+    shape = (len(images), c, h, w) if chw else (len(images), h, w)
+    out = torch.empty(shape, dtype=ref.dtype, device=ref.device)
+    esz = out.element_size()
+    pv = torch.tensor([pad_value], dtype=ref.dtype).view(_ELEM_TORCH[esz]).item()
+    pad = _ELEM_CT[esz](pv & ((1 << (8 * esz)) - 1))
+    ptrs, ext, kept = _ragged(images)
+    E.check(E.lib().rr_pad_images(ptrs, ext, len(images), c, h, w, esz, ctypes.byref(pad), E.ptr(out), _st()),
+            "rr_pad_images")
+    return out
+
+
+_ELEM_TORCH = {1: torch.uint8, 2: torch.int16, 4: torch.int32, 8: torch.int64}
+
+
 def resize_bilinear(img, scale_factor):
     """img: [C, H, W] (or a same-size batch [N, C, H, W]) float32 -> bilinear
     (align_corners=False) resize by scale_factor, output size floor(H*s) x

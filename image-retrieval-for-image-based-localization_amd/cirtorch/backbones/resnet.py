@@ -181,6 +181,21 @@ class ResNet(nn.Module):
         return run_step(t, st, residual, out)
 
     def _stem(self, plan, x, mean, std):
+        if isinstance(x, (list, tuple)):
+            # ragged batch (a PackedSequence of different sizes): the stem reads every
+            # image at its own address; the batch map is the max extent, padded with
+            # zeros before normalisation (utils/sequence.py:51, random_augmentation.py:102,174)
+            live = [t for t in x if t is not None]
+            if not live:
+                raise ValueError("at least one image of the batch must be non-None")
+            h = max(int(t.shape[-2]) for t in live)
+            w = max(int(t.shape[-1]) for t in live)
+            st = plan["stem"]
+            if plan["stem_fused"] is not None:
+                return _ops.stem_conv_pool_ragged(x, h, w, plan["stem_fused"], st.scale, st.shift, leaky=st.leaky,
+                                                  slope=st.slope, mean=mean, std=std)
+            t = _ops.image_to_nhwc_ragged(x, h, w, self.stem_cin(), self.engine_dtype, mean, std)
+            return _ops.maxpool2d(self._conv(t, st), 3, 2, 1)
         if x.dtype == torch.uint8 and plan["stem_fused"] is None:
             x = _ops.pixels_to_unit(x)  # pixels -> [0, 1] (to_tensor); the fused stem reads uint8 itself
         if plan["stem_fused"] is not None:
@@ -216,7 +231,9 @@ class ResNet(nn.Module):
         return t, pending
 
     def forward(self, x, normalize=None):
-        """x: [N, 3, H, W] float32 on the GPU, or uint8 pixels (read as x / 255) (already normalised unless
+        """x: [N, 3, H, W] float32 on the GPU, or uint8 pixels (read as x / 255), or a ragged batch -- a list
+        (PackedSequence) of [3, H_i, W_i] images, None allowed, run as the zero-padded max-extent batch
+        without building it -- (already normalised unless
         ``normalize=(mean, std)`` is given, which fuses cirtorch/utils/image.py
         ``normalize`` into the first kernel).  Returns OrderedDict mod1..mod5."""
         plan = self._plan or self._build_plan()

@@ -7,9 +7,11 @@ OrderedDict(ret_pred=Tensor[D, N])), with the reference semantics:
   * multi-scale: per-image bilinear resize (align_corners=False), recursive
     single-scale extraction, plain mean of the per-scale L2-normalised
     descriptors, no re-normalisation (``GF_net.py:20-40,74-92``);
-  * pad to the batch's max H, W top-left (``utils/sequence.py``), then
-    normalise (pads become -mean/std, ``random_augmentation.py:102,174``)
-    when an augment object carrying rgb_mean / rgb_std is attached;
+  * a PackedSequence goes to the body as a ragged batch: the stem reads every
+    image at its own address and pads to the max H, W top-left on the fly
+    (``utils/sequence.py`` semantics, no padded copy), then normalises (pads
+    become -mean/std, ``random_augmentation.py:102,174``) when an augment
+    object carrying rgb_mean / rgb_std is attached;
   * body -> ret_algo.inference(head, x) -> D x N.
 """
 
@@ -25,7 +27,6 @@ from ..algos.GF_algo import globalFeatureAlgo
 from ..backbones import resnet as _resnet
 from ..modules.heads.global_head import globalHead
 from ..utils.parallel import PackedSequence
-from ..utils.sequence import pad_packed_images
 
 from ..modules.utils import OUTPUT_DIM  # noqa: E402  (reference cirtorch/modules/utils.py:61-79)
 
@@ -107,10 +108,12 @@ class ImageRetrievalNet(nn.Module):
             pred = nn.functional.avg_pool1d(pred, kernel_size=len(scales)).squeeze(-1)
             return OrderedDict([("ret_loss", None)]), OrderedDict([("ret_pred", pred)])
         if isinstance(img, torch.Tensor):
-            if img.dtype == torch.uint8:  # pixels -> [0, 1] (to_tensor) for the resize / padding paths
+            if img.dtype == torch.uint8 and len(scales) > 1:  # pixels -> [0, 1] (to_tensor) for the resize
                 img = _ops.pixels_to_unit(img)
             img = PackedSequence(list(img)) if img.dim() == 4 else PackedSequence([img])
         if len(scales) > 1:
+            if img.dtype == torch.uint8:
+                img = PackedSequence([_ops.pixels_to_unit(t) if t is not None else None for t in img])
             preds = []
             for im in self._prepare_pyramid_inputs(img, scales):
                 _, pred = self.forward(img=im, scales=[1], do_prediction=True, do_loss=False)
@@ -119,8 +122,12 @@ class ImageRetrievalNet(nn.Module):
             pred = nn.functional.avg_pool1d(pred, kernel_size=len(scales)).squeeze(-1)
             return OrderedDict([("ret_loss", None)]), OrderedDict([("ret_pred", pred)])
 
-        padded, valid_size = pad_packed_images(img)
-        x = self.body(padded, normalize=self._normalizer())
+        # the ragged batch goes to the body as is: the stem reads each image at its own
+        # address and pads to the max extent on the fly (pad_packed_images semantics,
+        # utils/sequence.py:4-67, without writing the padded batch)
+        images = list(img)
+        x = self.body(images, normalize=self._normalizer())
+        valid_size = [tuple(t.shape[-2:]) if t is not None else (0, 0) for t in images]
         if do_prediction:
             ret_pred = self.ret_algo.inference(self.ret_head, x, valid_size)
         else:

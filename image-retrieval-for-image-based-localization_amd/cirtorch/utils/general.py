@@ -1,4 +1,6 @@
-"""Reference ``cirtorch/utils/general.py:1-27`` (data root, human-readable time)."""
+"""Upstream ``cirtorch.utils.general`` names ``scripts/test.py:18`` imports
+(reference ``cirtorch/utils/general.py:1-27``): the data root and a
+human-readable duration."""
 
 import os
 
@@ -12,15 +14,10 @@ def get_data_root():
 
 
 def htime(c):
-    c = round(c)
-    days = c // 86400
-    hours = c // 3600 % 24
-    minutes = c // 60 % 60
-    seconds = c % 60
-    if days > 0:
-        return "{:d}d {:d}h {:d}m {:d}s".format(days, hours, minutes, seconds)
-    if hours > 0:
-        return "{:d}h {:d}m {:d}s".format(hours, minutes, seconds)
-    if minutes > 0:
-        return "{:d}m {:d}s".format(minutes, seconds)
-    return "{:d}s".format(seconds)
+    """seconds -> "Dd Hh Mm Ss", starting at the largest non-zero unit ("5s", "2m 0s", ...)."""
+    minutes, secs = divmod(round(c), 60)
+    hours, mins = divmod(minutes, 60)
+    days, hrs = divmod(hours, 24)
+    fields = [(days, "d"), (hrs, "h"), (mins, "m"), (secs, "s")]
+    first = next((i for i, (v, _) in enumerate(fields[:-1]) if v > 0), len(fields) - 1)
+    return " ".join("%d%s" % f for f in fields[first:])

@@ -21,6 +21,27 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 int grid_cus();
 extern int g_grid_cap;
 
+// A ragged image batch (a cirtorch PackedSequence at the model boundary,
+// utils/parallel/packed_sequence.py:8-96): image i of a launch is [c][h_i][w_i]
+// at its own device address and the batch map is the max extent H x W.  Map
+// pixels outside image i's extent read as 0 -- the zero fill of
+// pad_packed_images (utils/sequence.py:51) -- BEFORE normalisation (the in-tree
+// order: random_augmentation.py:102 pads, :174 normalises), so no padded copy
+// of the batch is ever written.  Passed by value in the kernel arguments (one
+// 1-KiB table, graph-capturable, no host->device copy); the host splits a
+// longer batch into launches of at most RAGGED_MAX images.
+constexpr int RAGGED_MAX = 64;
+struct RaggedTab {
+    const void* p[RAGGED_MAX];
+    int h[RAGGED_MAX];
+    int w[RAGGED_MAX];
+};
+struct NoTab {};  // a same-size batch: one [n][c][H][W] buffer
+
+// Fill a table for images [i0, i0 + cnt) of a host (pointer, extent) list;
+// returns an error message or nullptr.
+const char* ragged_fill(RaggedTab& t, const void* const* srcs, const int* extents, int i0, int cnt, int h, int w);
+
 // Launch-error check: every entry point ends with this.
 inline int check_launch(const char* what) {
     hipError_t e = hipGetLastError();

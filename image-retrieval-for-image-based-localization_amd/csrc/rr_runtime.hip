@@ -81,6 +81,67 @@ __global__ void k_image_to_nhwc_bf16x8(const float* __restrict__ src, long long 
     dst[pix] = o;
 }
 
+// Ragged batch -> NHWC: one thread per pixel of the h x w batch map; image i's
+// planes are read at its own address (row stride w_i), map pixels outside its
+// extent read 0 and are then normalised like any other pixel (the pad-then-
+// normalise order of random_augmentation.py:102,174).  u8: x / 255 in IEEE
+// division (== to_tensor, == the LUT of pixels_to_unit).
+template <typename T, bool U8>
+__global__ void k_image_to_nhwc_ragged(RaggedTab rt, int c, int h, int w, NormParams np, int do_norm,
+                                       T* __restrict__ dst, int c_pad) {
+    const int hw = h * w;
+    const int img = blockIdx.y;
+    const int pix = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pix >= hw) return;
+    const int y = pix / w, x = pix - y * w;
+    const int hi = rt.h[img], wi = rt.w[img];
+    const bool in = y < hi && x < wi;
+    const long long plane = (long long)hi * wi, o = (long long)y * wi + x;
+    T* d = dst + ((long long)img * hw + pix) * c_pad;
+    for (int ch = 0; ch < c_pad; ++ch) {
+        float v = 0.f;
+        if (ch < c) {
+            if (in) {
+                if constexpr (U8) v = (float)((const unsigned char*)rt.p[img])[ch * plane + o] / 255.f;
+                else v = ((const float*)rt.p[img])[ch * plane + o];
+            }
+            if (do_norm) v = (v - np.mean[ch]) / np.stdv[ch];
+        }
+        d[ch] = DT<T>::from_f(v);
+    }
+}
+
+// pad_packed_images on the device: [n][c][h][w] elements of type E, image i's
+// [c][h_i][w_i] at the top-left, `pad` elsewhere.  One thread per output
+// element of one image (blockIdx.y), reads coalesced along each image row.
+template <typename E>
+__global__ void k_pad_images(RaggedTab rt, int c, int h, int w, E pad, E* __restrict__ dst) {
+    const int img = blockIdx.y;
+    const long long per = (long long)c * h * w;
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= per) return;
+    const int x = (int)(i % w);
+    const long long r = i / w;
+    const int y = (int)(r % h), ch = (int)(r / h);
+    const int hi = rt.h[img], wi = rt.w[img];
+    E v = pad;
+    if (y < hi && x < wi) v = ((const E*)rt.p[img])[((long long)ch * hi + y) * wi + x];
+    dst[img * per + i] = v;
+}
+
+const char* ragged_fill(RaggedTab& t, const void* const* srcs, const int* extents, int i0, int cnt, int h, int w) {
+    for (int j = 0; j < cnt; ++j) {
+        const int hi = extents[2 * (i0 + j)], wi = extents[2 * (i0 + j) + 1];
+        if (hi < 0 || wi < 0 || hi > h || wi > w) return "image extent outside the batch map";
+        if ((hi == 0) != (wi == 0)) return "image extent: both sides must be 0 (a None entry) or positive";
+        if (hi > 0 && !srcs[i0 + j]) return "null image pointer with a non-empty extent";
+        t.p[j] = hi > 0 ? srcs[i0 + j] : nullptr;
+        t.h[j] = hi;
+        t.w[j] = wi;
+    }
+    return nullptr;
+}
+
 // NHWC max-pool, 8 channels (16 B of bf16) per thread.
 __global__ void k_maxpool_nhwc_bf16x8(const uint4* __restrict__ x, int n, int h, int w, int c8, int k, int stride,
                                       int pad, uint4* __restrict__ y, int ho, int wo) {
@@ -296,6 +357,71 @@ int rr_image_to_nhwc(const float* src, int n, int c, int h, int w, const float* 
     else
         return fail(RR_EINVAL, "rr_image_to_nhwc: dtype");
     return check_launch("rr_image_to_nhwc");
+}
+
+int rr_image_to_nhwc_ragged(const void* const* srcs, const int* extents, int n, int c, int h, int w, int u8,
+                            const float* mean_host, const float* std_host, int do_normalize, void* dst, int c_pad,
+                            int dtype, void* stream) {
+    if (!srcs || !extents || !dst) return fail(RR_EINVAL, "rr_image_to_nhwc_ragged: null pointer");
+    if (c <= 0 || c > 4 || c_pad < c || n <= 0 || h <= 0 || w <= 0 || (long long)h * w >= (1ll << 31))
+        return fail(RR_EINVAL, "rr_image_to_nhwc_ragged: bad shape");
+    NormParams np{};
+    for (int i = 0; i < c; ++i) {
+        np.mean[i] = do_normalize ? mean_host[i] : 0.f;
+        np.stdv[i] = do_normalize ? std_host[i] : 1.f;
+    }
+    const int esz = dtype == RR_F32 ? 4 : 2;
+    if (dtype != RR_F32 && dtype != RR_BF16 && dtype != RR_F16) return fail(RR_EINVAL, "rr_image_to_nhwc_ragged: dtype");
+    for (int i0 = 0; i0 < n; i0 += RAGGED_MAX) {
+        const int cnt = n - i0 < RAGGED_MAX ? n - i0 : RAGGED_MAX;
+        RaggedTab t;
+        if (const char* e = ragged_fill(t, srcs, extents, i0, cnt, h, w))
+            return fail(RR_EINVAL, std::string("rr_image_to_nhwc_ragged: ") + e);
+        char* d = (char*)dst + (long long)i0 * h * w * c_pad * esz;
+        const dim3 grid(nblk((long long)h * w, 256), cnt);
+        auto launch = [&](auto kern, auto* out) {
+            hipLaunchKernelGGL(kern, grid, dim3(256), 0, as_stream(stream), t, c, h, w, np, do_normalize, out, c_pad);
+        };
+        if (dtype == RR_F32) {
+            if (u8) launch(k_image_to_nhwc_ragged<float, true>, (float*)d);
+            else launch(k_image_to_nhwc_ragged<float, false>, (float*)d);
+        } else if (dtype == RR_BF16) {
+            if (u8) launch(k_image_to_nhwc_ragged<bf16_t, true>, (bf16_t*)d);
+            else launch(k_image_to_nhwc_ragged<bf16_t, false>, (bf16_t*)d);
+        } else {
+            if (u8) launch(k_image_to_nhwc_ragged<f16_t, true>, (f16_t*)d);
+            else launch(k_image_to_nhwc_ragged<f16_t, false>, (f16_t*)d);
+        }
+    }
+    return check_launch("rr_image_to_nhwc_ragged");
+}
+
+int rr_pad_images(const void* const* srcs, const int* extents, int n, int c, int h, int w, int elem_bytes,
+                  const void* pad_value_host, void* dst, void* stream) {
+    if (!srcs || !extents || !dst || !pad_value_host) return fail(RR_EINVAL, "rr_pad_images: null pointer");
+    if (n <= 0 || c <= 0 || h <= 0 || w <= 0 || (long long)c * h * w >= (1ll << 40))
+        return fail(RR_EINVAL, "rr_pad_images: bad shape");
+    if (elem_bytes != 1 && elem_bytes != 2 && elem_bytes != 4 && elem_bytes != 8)
+        return fail(RR_EINVAL, "rr_pad_images: elem_bytes must be 1, 2, 4 or 8");
+    const long long per = (long long)c * h * w;
+    if ((per + 255) / 256 >= (1ll << 31)) return fail(RR_EINVAL, "rr_pad_images: image too large");
+    for (int i0 = 0; i0 < n; i0 += RAGGED_MAX) {
+        const int cnt = n - i0 < RAGGED_MAX ? n - i0 : RAGGED_MAX;
+        RaggedTab t;
+        if (const char* e = ragged_fill(t, srcs, extents, i0, cnt, h, w))
+            return fail(RR_EINVAL, std::string("rr_pad_images: ") + e);
+        char* d = (char*)dst + (long long)i0 * per * elem_bytes;
+        const dim3 grid(nblk(per, 256), cnt);
+        auto launch = [&](auto pad) {
+            typedef decltype(pad) E;
+            hipLaunchKernelGGL(k_pad_images<E>, grid, dim3(256), 0, as_stream(stream), t, c, h, w, pad, (E*)d);
+        };
+        if (elem_bytes == 1) launch(*(const uint8_t*)pad_value_host);
+        else if (elem_bytes == 2) launch(*(const uint16_t*)pad_value_host);
+        else if (elem_bytes == 4) launch(*(const uint32_t*)pad_value_host);
+        else launch(*(const uint64_t*)pad_value_host);
+    }
+    return check_launch("rr_pad_images");
 }
 
 int rr_maxpool2d(const void* x, int n, int h, int w, int c, int k, int stride, int pad, void* y, int ho, int wo,

@@ -55,8 +55,9 @@ __device__ __forceinline__ unsigned bf16_key2(unsigned w) {
     return w ^ (neg * 0x7FFFu);
 }
 
-template <int PH, int PW, typename HT, bool U8 = false>
-__global__ void __launch_bounds__(NT) k_stem_pool(StemArgs a, int tiles_w, int tiles_hw, int ntiles) {
+template <int PH, int PW, typename HT, bool U8 = false, typename TAB = NoTab>
+__global__ void __launch_bounds__(NT) k_stem_pool(StemArgs a, TAB rt, int tiles_w, int tiles_hw, int ntiles) {
+    constexpr bool RG = std::is_same<TAB, RaggedTab>::value;
     constexpr int SR = 2 * PH + 1, SC = 2 * PW + 1, NP = SR * SC, NF = (NP + 15) / 16;
     constexpr unsigned KNI = H16<HT>::NEG_INF ^ 0x7FFFu;  // order key of -inf (pool padding)
     constexpr unsigned KNI2 = KNI | (KNI << 16);
@@ -98,20 +99,31 @@ __global__ void __launch_bounds__(NT) k_stem_pool(StemArgs a, int tiles_w, int t
         int img, ph0, pw0;
         tile_origin(t, img, ph0, pw0);
         const int ir0 = 4 * ph0 - 5, ic0 = 4 * pw0 - 5;  // = 2 * (2 * p0 - 1) - 3
-        const long long ibase = (long long)img * 3 * plane;
+        // the image's own extent (ragged: its pixels at its own address; map pixels
+        // past it read 0 -- the batch pad, normalised in fill_store)
+        const void* ib = a.x;
+        int hi = H, wi = W;
+        long long ibase = (long long)img * 3 * plane, iplane = plane;
+        if constexpr (RG) {
+            ib = rt.p[img];
+            hi = rt.h[img];
+            wi = rt.w[img];
+            ibase = 0;
+            iplane = (long long)hi * wi;
+        }
 #pragma unroll
         for (int u = 0; u < SPT; ++u) {
             const int slot = tid + NT * u;
             const int r = slot / IC, c = slot - r * IC;
             const int ih = ir0 + r, iw = ic0 + c;
-            const bool ok = slot < NSLOT && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
-            const long long o = ok ? (long long)ih * W + iw : 0;
+            const bool ok = slot < NSLOT && (unsigned)ih < (unsigned)hi && (unsigned)iw < (unsigned)wi;
+            const long long o = ok ? (long long)ih * wi + iw : 0;
 #pragma unroll
             for (int ch = 0; ch < 3; ++ch) {
                 if constexpr (U8)  // IEEE division: the same float as torch's / numpy's x / 255
-                    pf[u][ch] = ok ? (float)((const unsigned char*)a.x)[ibase + ch * plane + o] / 255.f : 0.f;
+                    pf[u][ch] = ok ? (float)((const unsigned char*)ib)[ibase + ch * iplane + o] / 255.f : 0.f;
                 else
-                    pf[u][ch] = ok ? ((const float*)a.x)[ibase + ch * plane + o] : 0.f;
+                    pf[u][ch] = ok ? ((const float*)ib)[ibase + ch * iplane + o] : 0.f;
             }
         }
     };
@@ -489,8 +501,9 @@ __global__ void __launch_bounds__(NT) k_stem_pool2(StemArgs a, int tiles_w, int 
 // of the normalised value of each byte (x / 255 in IEEE division, then the
 // same normalisation), computed once per block.  Same values as v2 bit for
 // bit when the swapped MFMA accumulates in the same order.
-template <typename HT, bool U8, int NPART>
-__global__ void __launch_bounds__(NT) k_stem_pool3(StemArgs a, int tiles_w, int tiles_hw, int ntiles) {
+template <typename HT, bool U8, int NPART, typename TAB = NoTab>
+__global__ void __launch_bounds__(NT) k_stem_pool3(StemArgs a, TAB rt, int tiles_w, int tiles_hw, int ntiles) {
+    constexpr bool RG = std::is_same<TAB, RaggedTab>::value;
     constexpr int PH = 8, PW = 56, SRN = 2 * PH + 1, CB = 14;
     constexpr int IR = 2 * (SRN - 1) + 7;            // 39 input rows
     constexpr int SCN = CB * 7 + 16;                 // 114 stem columns
@@ -555,9 +568,20 @@ __global__ void __launch_bounds__(NT) k_stem_pool3(StemArgs a, int tiles_w, int 
         const int ir0 = 4 * ph0 - 5, ic0 = 4 * pw0 - 5;
         constexpr int ESZ = U8 ? 1 : 4;
         constexpr unsigned OOBO = 0x80000000u;
-        const char* ib = (const char*)a.x + (long long)img * 3 * plane * ESZ;
+        // the image's own extent and planes (ragged: at its own address; map
+        // pixels past its extent read 0 -- the batch pad, normalised in fill_store)
+        const char* ib;
+        int hi = H, wi = W;
+        if constexpr (RG) {
+            ib = (const char*)rt.p[img];
+            hi = rt.h[img];
+            wi = rt.w[img];
+        } else {
+            ib = (const char*)a.x + (long long)img * 3 * plane * ESZ;
+        }
+        const int iplane = hi * wi;
         const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc((void*)ib, (short)0, (int)(3 * plane * ESZ), 0x00020000);
+            __builtin_amdgcn_make_buffer_rsrc((void*)ib, (short)0, (int)(3 * iplane * ESZ), 0x00020000);
 #pragma unroll
         for (int uu = 0; uu < PH1; ++uu) {
             const int u = half * PH1 + uu;
@@ -567,13 +591,13 @@ __global__ void __launch_bounds__(NT) k_stem_pool3(StemArgs a, int tiles_w, int 
             const int kk = k < NPAIR ? k : NPAIR - 1;
             const int r = kk / HIC, c = 2 * (kk - r * HIC);
             const int ih = ir0 + r, iw = ic0 + c;
-            const bool rok = (unsigned)ih < (unsigned)H;
-            const int o = (ih * W + iw) * ESZ;
-            const unsigned off0 = rok && (unsigned)iw < (unsigned)W ? (unsigned)o : OOBO;
-            const unsigned off1 = rok && (unsigned)(iw + 1) < (unsigned)W ? (unsigned)(o + ESZ) : OOBO;
+            const bool rok = (unsigned)ih < (unsigned)hi;
+            const int o = (ih * wi + iw) * ESZ;
+            const unsigned off0 = rok && (unsigned)iw < (unsigned)wi ? (unsigned)o : OOBO;
+            const unsigned off1 = rok && (unsigned)(iw + 1) < (unsigned)wi ? (unsigned)(o + ESZ) : OOBO;
 #pragma unroll
             for (int ch = 0; ch < 3; ++ch) {
-                const unsigned po = (unsigned)(ch * (int)plane * ESZ);
+                const unsigned po = (unsigned)(ch * iplane * ESZ);
                 if constexpr (U8) {
                     pf[uu][2 * ch] = ch * 256 + (int)__builtin_amdgcn_raw_buffer_load_b8(rs, (int)(off0 + po), 0, 0);
                     pf[uu][2 * ch + 1] = ch * 256 + (int)__builtin_amdgcn_raw_buffer_load_b8(rs, (int)(off1 + po), 0, 0);
@@ -753,19 +777,73 @@ int g_stem_mode = 2;  // rr_set_tuning(RR_TUNE_STEM): 2 swapped-operand lane-loc
                       // 1 pool-before-epilogue kernel (v2), 0 k_stem_pool
 }
 
+// One launch over a same-size batch (TAB = NoTab, a.x = the [n][3][h][w] buffer)
+// or over <= RAGGED_MAX images of a ragged batch (TAB = RaggedTab).
+template <bool U8, typename TAB>
+static void stem_launch(const StemArgs& a, const TAB& rt, int dtype, hipStream_t st) {
+    constexpr bool RG = std::is_same<TAB, RaggedTab>::value;
+    const int g_stem_cus = grid_cus();
+    if (g_stem_mode >= 1 && a.ho % 2 == 0 && a.wo % 2 == 0) {  // v2/v3 handle the even stem maps (borders top / left)
+        constexpr int PH = 8, PW = 56;
+        const int tiles_w = (a.wp + PW - 1) / PW, tiles_h = (a.hp + PH - 1) / PH;
+        const int ntiles = a.n * tiles_h * tiles_w;
+        const int grid = ntiles < g_stem_cus ? ntiles : g_stem_cus;
+        if (g_stem_mode >= 2 || RG) {  // 2: patch fill in 3 parts (default), 3: 2 parts, 4: 5 parts
+            auto launch = [&](auto kern) {
+                hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), 0, st, a, rt, tiles_w, tiles_w * tiles_h, ntiles);
+            };
+            if (dtype == RR_F16) {
+                if (g_stem_mode == 3) launch(k_stem_pool3<f16_t, U8, 2, TAB>);
+                else if (g_stem_mode == 4) launch(k_stem_pool3<f16_t, U8, 5, TAB>);
+                else launch(k_stem_pool3<f16_t, U8, 3, TAB>);
+            } else {
+                if (g_stem_mode == 3) launch(k_stem_pool3<bf16_t, U8, 2, TAB>);
+                else if (g_stem_mode == 4) launch(k_stem_pool3<bf16_t, U8, 5, TAB>);
+                else launch(k_stem_pool3<bf16_t, U8, 3, TAB>);
+            }
+            return;
+        }
+        if constexpr (!RG) {
+            if (dtype == RR_F16)
+                hipLaunchKernelGGL((k_stem_pool2<f16_t, U8>), dim3(grid), dim3(NT), 0, st, a, tiles_w,
+                                   tiles_w * tiles_h, ntiles);
+            else
+                hipLaunchKernelGGL((k_stem_pool2<bf16_t, U8>), dim3(grid), dim3(NT), 0, st, a, tiles_w,
+                                   tiles_w * tiles_h, ntiles);
+        }
+        return;
+    }
+    constexpr int PH = 4, PW = 32;
+    const int tiles_w = (a.wp + PW - 1) / PW, tiles_h = (a.hp + PH - 1) / PH;
+    const int ntiles = a.n * tiles_h * tiles_w;
+    const int grid = ntiles < g_stem_cus ? ntiles : g_stem_cus;
+    if (dtype == RR_F16)
+        hipLaunchKernelGGL((k_stem_pool<PH, PW, f16_t, U8, TAB>), dim3(grid), dim3(NT), 0, st, a, rt, tiles_w,
+                           tiles_w * tiles_h, ntiles);
+    else
+        hipLaunchKernelGGL((k_stem_pool<PH, PW, bf16_t, U8, TAB>), dim3(grid), dim3(NT), 0, st, a, rt, tiles_w,
+                           tiles_w * tiles_h, ntiles);
+}
+
+// x: a same-size [n][3][h][w] batch, or (srcs != nullptr) a ragged batch whose
+// image i is [3][extents[2i]][extents[2i+1]] at srcs[i], padded to h x w.
 template <bool U8>
-static int stem_conv_pool(const void* x, int n, int h, int w, const float* mean_host, const float* std_host,
-                          int do_normalize, const void* wpk, const float* scale, const float* shift, int act,
-                          float slope, void* y, int hp, int wp, int dtype, void* stream) {
-    if (dtype != RR_BF16 && dtype != RR_F16) return fail(RR_EINVAL, "rr_stem_conv_pool: bf16 / fp16 only");
-    if (!x || !wpk || !scale || !shift || !y) return fail(RR_EINVAL, "rr_stem_conv_pool: null pointer");
-    if (n <= 0 || h <= 0 || w <= 0) return fail(RR_EINVAL, "rr_stem_conv_pool: bad shape");
+static int stem_conv_pool(const void* x, const void* const* srcs, const int* extents, int n, int h, int w,
+                          const float* mean_host, const float* std_host, int do_normalize, const void* wpk,
+                          const float* scale, const float* shift, int act, float slope, void* y, int hp, int wp,
+                          int dtype, void* stream) {
+    const char* fn = srcs ? "rr_stem_conv_pool_ragged" : "rr_stem_conv_pool";
+    auto err = [&](const char* m) { return fail(RR_EINVAL, std::string(fn) + ": " + m); };
+    if (dtype != RR_BF16 && dtype != RR_F16) return err("bf16 / fp16 only");
+    if ((!x && !srcs) || (srcs && !extents) || !wpk || !scale || !shift || !y) return err("null pointer");
+    if (n <= 0 || h <= 0 || w <= 0) return err("bad shape");
     const int ho = (h + 2 * 3 - 7) / 2 + 1, wo = (w + 2 * 3 - 7) / 2 + 1;
-    if (ho <= 0 || wo <= 0) return fail(RR_EINVAL, "rr_stem_conv_pool: image smaller than the kernel");
+    if (ho <= 0 || wo <= 0) return err("image smaller than the kernel");
     if (hp != (ho + 2 - 3) / 2 + 1 || wp != (wo + 2 - 3) / 2 + 1)
-        return fail(RR_EINVAL, "rr_stem_conv_pool: output size must be the 3x3/s2/p1 pool of the stem map");
-    if ((long long)n * 3 * h * w >= (1ll << 40)) return fail(RR_EINVAL, "rr_stem_conv_pool: input too large");
-    if (act != RR_ACT_IDENTITY && act != RR_ACT_LEAKY) return fail(RR_EINVAL, "rr_stem_conv_pool: act");
+        return err("output size must be the 3x3/s2/p1 pool of the stem map");
+    if ((long long)3 * h * w * (U8 ? 1 : 4) >= (1ll << 31)) return err("image too large (32-bit buffer offsets)");
+    if ((long long)n * ((hp + 3) / 4) * ((wp + 31) / 32) >= (1ll << 31)) return err("too many tiles");
+    if (act != RR_ACT_IDENTITY && act != RR_ACT_LEAKY) return err("act");
     StemArgs a;
     a.x = x;
     a.w = (const uint4*)wpk;
@@ -779,64 +857,47 @@ static int stem_conv_pool(const void* x, int n, int h, int w, const float* mean_
         a.rstd[c] = do_normalize ? (float)(1.0 / (double)std_host[c]) : 1.f;
     }
     a.leaky = act == RR_ACT_LEAKY;
-    if (a.leaky && !(slope >= 0.f && slope <= 1.f)) return fail(RR_EINVAL, "rr_stem_conv_pool: leaky slope must be in [0, 1]");
+    if (a.leaky && !(slope >= 0.f && slope <= 1.f)) return err("leaky slope must be in [0, 1]");
     a.slope = slope;
-    const int g_stem_cus = grid_cus();
-    if (g_stem_mode >= 1 && ho % 2 == 0 && wo % 2 == 0) {  // v2/v3 handle the even stem maps (borders top / left)
-        constexpr int PH = 8, PW = 56;
-        const int tiles_w = (wp + PW - 1) / PW, tiles_h = (hp + PH - 1) / PH;
-        const long long ntiles = (long long)n * tiles_h * tiles_w;
-        if (ntiles >= (1ll << 31)) return fail(RR_EINVAL, "rr_stem_conv_pool: too many tiles");
-        const int grid = (int)(ntiles < g_stem_cus ? ntiles : g_stem_cus);
-        if (g_stem_mode >= 2) {  // 2: patch fill in 3 parts (default), 3: 2 parts, 4: 5 parts
-            auto launch = [&](auto kern) {
-                hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), 0, as_stream(stream), a, tiles_w, tiles_w * tiles_h,
-                                   (int)ntiles);
-            };
-            if (dtype == RR_F16) {
-                if (g_stem_mode == 3) launch(k_stem_pool3<f16_t, U8, 2>);
-                else if (g_stem_mode == 4) launch(k_stem_pool3<f16_t, U8, 5>);
-                else launch(k_stem_pool3<f16_t, U8, 3>);
-            } else {
-                if (g_stem_mode == 3) launch(k_stem_pool3<bf16_t, U8, 2>);
-                else if (g_stem_mode == 4) launch(k_stem_pool3<bf16_t, U8, 5>);
-                else launch(k_stem_pool3<bf16_t, U8, 3>);
-            }
-            return check_launch("rr_stem_conv_pool");
-        }
-        if (dtype == RR_F16)
-            hipLaunchKernelGGL((k_stem_pool2<f16_t, U8>), dim3(grid), dim3(NT), 0, as_stream(stream), a, tiles_w,
-                               tiles_w * tiles_h, (int)ntiles);
-        else
-            hipLaunchKernelGGL((k_stem_pool2<bf16_t, U8>), dim3(grid), dim3(NT), 0, as_stream(stream), a, tiles_w,
-                               tiles_w * tiles_h, (int)ntiles);
-        return check_launch("rr_stem_conv_pool");
+    if (!srcs) {
+        stem_launch<U8>(a, NoTab{}, dtype, as_stream(stream));
+        return check_launch(fn);
     }
-    constexpr int PH = 4, PW = 32;
-    const int tiles_w = (wp + PW - 1) / PW, tiles_h = (hp + PH - 1) / PH;
-    const long long ntiles = (long long)n * tiles_h * tiles_w;
-    if (ntiles >= (1ll << 31)) return fail(RR_EINVAL, "rr_stem_conv_pool: too many tiles");
-    const int grid = (int)(ntiles < g_stem_cus ? ntiles : g_stem_cus);
-    if (dtype == RR_F16)
-        hipLaunchKernelGGL((k_stem_pool<PH, PW, f16_t, U8>), dim3(grid), dim3(NT), 0, as_stream(stream), a, tiles_w,
-                           tiles_w * tiles_h, (int)ntiles);
-    else
-        hipLaunchKernelGGL((k_stem_pool<PH, PW, bf16_t, U8>), dim3(grid), dim3(NT), 0, as_stream(stream), a, tiles_w,
-                           tiles_w * tiles_h, (int)ntiles);
-    return check_launch("rr_stem_conv_pool");
+    for (int i0 = 0; i0 < n; i0 += RAGGED_MAX) {
+        const int cnt = n - i0 < RAGGED_MAX ? n - i0 : RAGGED_MAX;
+        RaggedTab t;
+        if (const char* e = ragged_fill(t, srcs, extents, i0, cnt, h, w)) return err(e);
+        StemArgs ac = a;
+        ac.x = nullptr;
+        ac.n = cnt;
+        ac.y = (bf16_t*)y + (long long)i0 * hp * wp * 64;
+        stem_launch<U8>(ac, t, dtype, as_stream(stream));
+    }
+    return check_launch(fn);
 }
 
 extern "C" int rr_stem_conv_pool(const float* x, int n, int h, int w, const float* mean_host, const float* std_host,
                                  int do_normalize, const void* wpk, const float* scale, const float* shift, int act,
                                  float slope, void* y, int hp, int wp, int dtype, void* stream) {
-    return stem_conv_pool<false>(x, n, h, w, mean_host, std_host, do_normalize, wpk, scale, shift, act, slope, y, hp,
-                                 wp, dtype, stream);
+    return stem_conv_pool<false>(x, nullptr, nullptr, n, h, w, mean_host, std_host, do_normalize, wpk, scale, shift,
+                                 act, slope, y, hp, wp, dtype, stream);
 }
 
 extern "C" int rr_stem_conv_pool_u8(const unsigned char* x, int n, int h, int w, const float* mean_host,
                                     const float* std_host, int do_normalize, const void* wpk, const float* scale,
                                     const float* shift, int act, float slope, void* y, int hp, int wp, int dtype,
                                     void* stream) {
-    return stem_conv_pool<true>(x, n, h, w, mean_host, std_host, do_normalize, wpk, scale, shift, act, slope, y, hp,
-                                wp, dtype, stream);
+    return stem_conv_pool<true>(x, nullptr, nullptr, n, h, w, mean_host, std_host, do_normalize, wpk, scale, shift,
+                                act, slope, y, hp, wp, dtype, stream);
+}
+
+extern "C" int rr_stem_conv_pool_ragged(const void* const* srcs, const int* extents, int n, int h, int w, int u8,
+                                        const float* mean_host, const float* std_host, int do_normalize,
+                                        const void* wpk, const float* scale, const float* shift, int act, float slope,
+                                        void* y, int hp, int wp, int dtype, void* stream) {
+    if (!srcs) return fail(RR_EINVAL, "rr_stem_conv_pool_ragged: null image table");
+    return u8 ? stem_conv_pool<true>(nullptr, srcs, extents, n, h, w, mean_host, std_host, do_normalize, wpk, scale,
+                                     shift, act, slope, y, hp, wp, dtype, stream)
+              : stem_conv_pool<false>(nullptr, srcs, extents, n, h, w, mean_host, std_host, do_normalize, wpk, scale,
+                                      shift, act, slope, y, hp, wp, dtype, stream);
 }

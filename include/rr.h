@@ -134,6 +134,34 @@ int rr_stem_conv_pool_u8(const unsigned char* x, int n, int h, int w, const floa
                          const float* shift, int act, float slope, void* y, int hp, int wp, int dtype,
                          void* stream);
 
+/* ---- ragged image batches (a PackedSequence of different-size images) ----
+ * Replace pad_packed_images (cirtorch/utils/sequence.py:4-67) + normalize
+ * (utils/image.py:125) on a cirtorch.utils.parallel.PackedSequence
+ * (utils/parallel/packed_sequence.py:8-96) feeding the body: image i is
+ * [c][h_i][w_i] at its own DEVICE address srcs[i] (NULL with h_i = w_i = 0 for
+ * a None entry); `extents` is a HOST array {h_0, w_0, h_1, w_1, ...}; the
+ * batch map is h x w (>= every extent).  Map pixels outside image i read as 0
+ * (the reference's top-left zero pad) BEFORE normalisation -- in-tree order,
+ * random_augmentation.py:102 then :174 -- so a pad becomes -mean/std when
+ * do_normalize.  No padded copy of the batch is written; `srcs` are read
+ * directly.  u8: srcs are uint8 pixels read as x / 255 (to_tensor), else
+ * float32.  Any n (split internally into launches of <= 64 images). */
+int rr_image_to_nhwc_ragged(const void* const* srcs, const int* extents, int n, int c, int h, int w, int u8,
+                            const float* mean_host, const float* std_host, int do_normalize,
+                            void* dst, int c_pad, int dtype, void* stream);
+/* The fused stem (rr_stem_conv_pool) on a ragged batch; y is [n][hp][wp][64]
+ * of the h x w batch map.  Results equal rr_stem_conv_pool(_u8) on the padded
+ * batch bit for bit. */
+int rr_stem_conv_pool_ragged(const void* const* srcs, const int* extents, int n, int h, int w, int u8,
+                             const float* mean_host, const float* std_host, int do_normalize, const void* wpk,
+                             const float* scale, const float* shift, int act, float slope, void* y, int hp, int wp,
+                             int dtype, void* stream);
+/* pad_packed_images itself (utils/sequence.py:4-67) for device tensors: one
+ * launch writes the [n][c][h][w] padded batch (elements of elem_bytes = 1, 2,
+ * 4 or 8 bytes; pad_value points to one HOST element) from the ragged list. */
+int rr_pad_images(const void* const* srcs, const int* extents, int n, int c, int h, int w, int elem_bytes,
+                  const void* pad_value_host, void* dst, void* stream);
+
 /* Bilinear resize, align_corners=False, NCHW float32 (one image).
  * Replaces nn.functional.interpolate(scale_factor=s, mode='bilinear',
  * align_corners=False) of the multi-scale pyramid (cirtorch/models/GF_net.py:32-35). */

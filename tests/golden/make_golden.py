@@ -236,6 +236,34 @@ def gen_net(arch, res, n, seed, scales_list, fname, mixed=None, local=None):
     np.savez_compressed(os.path.join(HERE, fname), **out)
 
 
+def gen_mixed(arch, sizes, seed, fname):
+    """A ragged batch (PackedSequence of different sizes) through the reference, in
+    both orders the reference code has: (a) augment=None on pre-normalised images:
+    ImageRetrievalNet pads the normalised images with zeros (GF_net.py:99 ->
+    sequence.py:4-67); (b) the in-tree augment order, pad first then normalise
+    (random_augmentation.py:102 then :174): the reference pad_packed_images on the
+    raw images, the reference normalize on the padded batch, then the net."""
+    from cirtorch.utils.sequence import pad_packed_images as R_pad
+    bias = centering_bias(arch)
+    net, _ = reference_net(arch, head_bias=bias)
+    imgs = [data.structured_images(1, h, w, seed=seed + i)[0] for i, (h, w) in enumerate(sizes)]
+    onet = obb.OracleNet(arch, weights.backbone_state(arch),
+                         dict(weights.head_state(weights.OUTPUT_DIM[arch]), **{"whiten.bias": bias}))
+    out = {"head_bias": bias, "seed": np.int64(seed), "mixed_sizes": np.array(sizes)}
+    out["desc_mixed"] = run_ref(net, imgs)
+    nimgs = [obb.normalize_images(torch.from_numpy(im)) for im in imgs]
+    check_close(arch + " mixed (normalise, pad)", out["desc_mixed"],
+                onet.forward(nimgs, normalize=False).numpy(), 1e-4)
+    padded, _ = R_pad(PackedSequence([torch.from_numpy(im) for im in imgs]))
+    padded = R_normalize(padded, MEAN, STD)
+    with torch.no_grad():
+        _, pred = net(img=PackedSequence(list(padded)), scales=[1], do_prediction=True)
+    out["desc_mixed_padnorm"] = pred["ret_pred"].numpy()
+    check_close(arch + " mixed (pad, normalise)", out["desc_mixed_padnorm"],
+                onet.forward([torch.from_numpy(im) for im in imgs], normalize=True).numpy(), 1e-4)
+    np.savez_compressed(os.path.join(HERE, fname), **out)
+
+
 # ----------------------------------------------------------------------------- G4
 def gen_knn():
     out = {}
@@ -414,6 +442,8 @@ GENERATORS = {
     "r101ms": lambda: gen_net("resnet101", (768, 1024), 1, 2301, [(1,), (0.5, 1, 2)], "r101ms.npz"),
     # config 5: R152 at 768x1024 + the local head on mod3
     "r152": lambda: gen_net("resnet152", (768, 1024), 1, 2401, [(1,)], "r152.npz", local=("mod3", 512, 128, 2402)),
+    # a2: a ragged R50 batch at 768x1024 / 640x960 / 700x1000 (both pad orders)
+    "r50mixed": lambda: gen_mixed("resnet50", [(768, 1024), (640, 960), (700, 1000)], 2501, "r50mixed.npz"),
     "knn": lambda: gen_knn(),
     "map": lambda: gen_map(),
     "whiten": lambda: gen_whiten(),

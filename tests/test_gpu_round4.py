@@ -1,0 +1,157 @@
+"""Round-4 GPU tests: the ragged image batch.
+
+A PackedSequence of different-size images goes to the body as a ragged table
+(rr_stem_conv_pool_ragged / rr_image_to_nhwc_ragged): the stem reads each
+image at its own address and pads to the max extent on the fly.  Checked
+  * against the reference (tests/golden/r50mixed.npz: R50 at 768x1024,
+    640x960, 700x1000, both pad orders the reference code has), fp32 at the
+    north-star bar 1 - 1e-4 and fp16 at its documented bar;
+  * bit for bit against the same engine on the explicitly padded batch
+    (ragged and padded runs must be the same computation);
+  * rr_pad_images (pad_packed_images on device tensors) against the host path.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import cosines, golden
+
+pytestmark = pytest.mark.gpu
+
+FP32_COS = 1 - 1e-4
+FP16_COS = 1 - 5e-4
+BF16_COS = 1 - 2e-3
+MEAN, STD = [0.485, 0.456, 0.406], [0.229, 0.224, 0.225]
+
+
+def _net(arch, head_bias, precision, cuda, normalize):
+    from cirtorch.models.GF_net import make_net
+    from oracle import weights
+    net = make_net(arch, precision=precision, mean=MEAN if normalize else None, std=STD if normalize else None)
+    missing, unexpected = net.body.load_state_dict(
+        {k: torch.from_numpy(v) for k, v in weights.backbone_state(arch).items()}, strict=False)
+    assert not unexpected and not missing
+    hs = weights.head_state(weights.OUTPUT_DIM[arch])
+    hs["whiten.bias"] = head_bias
+    net.ret_head.load_state_dict({k: torch.from_numpy(v) for k, v in hs.items()})
+    return net.to(cuda).eval()
+
+
+def _mixed_images(g):
+    from oracle import data
+    sizes = [tuple(int(v) for v in hw) for hw in g["mixed_sizes"]]
+    return [data.structured_images(1, h, w, seed=int(g["seed"]) + i)[0] for i, (h, w) in enumerate(sizes)]
+
+
+@pytest.mark.parametrize("precision", ["fp32", "fp16", "bf16"])
+def test_r50_ragged_batch_vs_reference(cuda, precision):
+    """the ragged R50 batch, both pad orders, vs the reference golden"""
+    from oracle import backbone as obb
+    g = golden("r50mixed.npz")
+    imgs = _mixed_images(g)
+    bar = {"fp32": FP32_COS, "fp16": FP16_COS, "bf16": BF16_COS}[precision]
+    # (a) augment=None on pre-normalised images: the pads are 0 in the normalised domain
+    net = _net("resnet50", g["head_bias"], precision, cuda, normalize=False)
+    got = net.extract([obb.normalize_images(torch.from_numpy(im)).to(cuda) for im in imgs]).cpu().numpy()
+    cos = cosines(got, g["desc_mixed"])
+    print(precision, "normalise->pad cos", cos)
+    assert cos.min() >= bar
+    # (b) the in-tree order: pad with 0 first, then normalise (pads become -mean/std)
+    net = _net("resnet50", g["head_bias"], precision, cuda, normalize=True)
+    got = net.extract([torch.from_numpy(im).to(cuda) for im in imgs]).cpu().numpy()
+    cos = cosines(got, g["desc_mixed_padnorm"])
+    print(precision, "pad->normalise cos", cos)
+    assert cos.min() >= bar
+
+
+def _padded(imgs, pad=0):
+    h = max(t.shape[-2] for t in imgs)
+    w = max(t.shape[-1] for t in imgs)
+    out = imgs[0].new_full((len(imgs), imgs[0].shape[0], h, w), pad)
+    for i, t in enumerate(imgs):
+        out[i, :, :t.shape[-2], :t.shape[-1]] = t
+    return out
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp16", "fp32"])
+@pytest.mark.parametrize("sizes", [[(96, 128), (80, 100), (64, 128)],     # even stem map: fused v3 stem
+                                   [(100, 130), (90, 120), (75, 130)]])   # odd stem map (wo = 65)
+@pytest.mark.parametrize("u8", [False, True])
+def test_ragged_equals_padded_bitwise(cuda, precision, sizes, u8):
+    """the ragged stem and the padded-batch stem are the same computation: bit-identical
+    descriptors (the pad read as 0 before normalisation, like the padded tensor's zeros)"""
+    from cirtorch.models.GF_net import make_net
+    from cirtorch.models.init import random_init_
+    net = make_net("resnet18", precision=precision, mean=MEAN, std=STD)
+    random_init_(net, seed=4)
+    net = net.to(cuda).eval()
+    g = torch.Generator(device=cuda).manual_seed(9)
+    if u8:
+        imgs = [torch.randint(0, 256, (3, h, w), generator=g, device=cuda, dtype=torch.uint8) for h, w in sizes]
+    else:
+        imgs = [torch.rand((3, h, w), generator=g, device=cuda) for h, w in sizes]
+    ragged = net.extract(imgs)
+    padded = net.extract(_padded(imgs))
+    assert torch.equal(ragged, padded)
+
+
+def test_ragged_none_entry_and_long_batch(cuda):
+    """> 64 images (several ragged launches) and a None entry (all pad) equal the padded batch"""
+    from cirtorch.models.GF_net import make_net
+    from cirtorch.models.init import random_init_
+    from cirtorch.utils.parallel import PackedSequence
+    net = make_net("resnet18", precision="fp16", mean=MEAN, std=STD)
+    random_init_(net, seed=5)
+    net = net.to(cuda).eval()
+    g = torch.Generator(device=cuda).manual_seed(11)
+    sizes = [(64 - 2 * (i % 7), 96 - 4 * (i % 5)) for i in range(70)]
+    imgs = [torch.rand((3, h, w), generator=g, device=cuda) for h, w in sizes]
+    assert torch.equal(net.extract(imgs), net.extract(_padded(imgs)))
+    with torch.no_grad():
+        _, pred = net(img=PackedSequence([imgs[0], None, imgs[1]]))
+        zero = torch.zeros_like(imgs[0])
+        ref = net.extract(_padded([imgs[0], zero, imgs[1]]))
+    assert torch.equal(pred["ret_pred"], ref)
+
+
+def test_ragged_stage_maps_equal_padded(cuda):
+    """every stage map of the ragged batch equals the padded batch's (fp32 and fp16)"""
+    from cirtorch.models.GF_net import make_net
+    from cirtorch.models.init import random_init_
+    g = torch.Generator(device=cuda).manual_seed(12)
+    imgs = [torch.rand((3, h, w), generator=g, device=cuda) for h, w in [(120, 160), (96, 150), (128, 100)]]
+    for prec in ("fp32", "fp16"):
+        net = make_net("resnet50", precision=prec, mean=MEAN, std=STD)
+        random_init_(net, seed=6)
+        net = net.to(cuda).eval()
+        with torch.no_grad():
+            a = net.body(imgs, normalize=(MEAN, STD))
+            b = net.body(_padded(imgs), normalize=(MEAN, STD))
+        for k in a:
+            assert torch.equal(a[k], b[k]), (prec, k)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.uint8, torch.int64])
+def test_pad_packed_images_device_equals_host(cuda, dtype):
+    from cirtorch.utils.parallel import PackedSequence
+    from cirtorch.utils.sequence import pad_packed_images, pack_padded_images
+    r = np.random.default_rng(3)
+    shapes = [(3, 5, 7), (3, 6, 4), None, (3, 2, 9)]
+    host = [None if s is None else torch.from_numpy((r.random(s) * 100).astype(np.float64)).to(dtype) for s in shapes]
+    for snap in (None, 4):
+        for pad in (0, 7):
+            ph, sh = pad_packed_images(PackedSequence(host), pad_value=pad, snap_size_to=snap)
+            pd, sd = pad_packed_images(PackedSequence([None if t is None else t.to(cuda) for t in host]),
+                                       pad_value=pad, snap_size_to=snap)
+            assert pd.is_cuda and torch.equal(pd.cpu(), ph)
+            assert [tuple(s) for s in sd] == [tuple(s) for s in sh]
+    back = pack_padded_images(pd, sd)
+    for t, b in zip(host, back):
+        if t is not None:
+            assert torch.equal(b.cpu(), t)
+    # 2D entries
+    h2 = [torch.rand(4, 6), torch.rand(5, 3)]
+    ph, _ = pad_packed_images(PackedSequence(h2), pad_value=-1.0)
+    pd, _ = pad_packed_images(PackedSequence([t.to(cuda) for t in h2]), pad_value=-1.0)
+    assert torch.equal(pd.cpu(), ph) and ph.shape == (2, 5, 6)
