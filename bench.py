@@ -2,7 +2,9 @@
 """Extract-and-match benchmark (BASELINE.json metric).
 
 One step (per rank): extract B synthetic 3x768x1024 images with ResNet50-GeM
-(+ whitening head) in bf16 on the MFMA engine, all-gather the B x world query
+(+ whitening head) in fp16 on the MFMA engine (the precision that meets the
+north-star descriptor bar; bf16, BASELINE config 2, is the e2e_bf16 sub-line),
+all-gather the B x world query
 descriptors, search them (top-100 cosine kNN, exact ordering) against a
 1M x 2048 database sharded over the ranks (per-shard top-k -> RCCL all-gather
 -> on-GPU merge).  Per-rank work is fixed as ranks grow (images per rank,
@@ -50,7 +52,9 @@ def parse():
     ap.add_argument("--height", type=int, default=768)
     ap.add_argument("--width", type=int, default=1024)
     ap.add_argument("--arch", default="resnet50")
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp16", "fp32"])
+    ap.add_argument("--precision", default="fp16", choices=["bf16", "fp16", "fp32"],
+                    help="headline precision: fp16 meets the north-star descriptor bar (cosine >= 1 - 1e-4 vs the "
+                         "reference); bf16 (BASELINE config 2) runs as the e2e_bf16 sub-line")
     ap.add_argument("--db-rows", type=int, default=1_000_000)
     ap.add_argument("--dim", type=int, default=2048)
     ap.add_argument("--k", type=int, default=100)
@@ -84,8 +88,14 @@ def parse():
     ap.add_argument("--extract-priority", type=int, default=int(os.environ.get("RR_BENCH_PRIO", "0")),
                     help="1: run the extraction on a high-priority stream (the overlapped search keeps the default)")
     ap.add_argument("--tune", default="", help="developer A/B: rr_set_tuning pairs key=value[,key=value]")
-    ap.add_argument("--fp16-steps", type=int, default=10,
-                    help="steps of the fp16 end-to-end line (e2e_fp16; 0 = skip)")
+    ap.add_argument("--alt-steps", "--fp16-steps", dest="alt_steps", type=int, default=10,
+                    help="steps of the end-to-end line in the other 16-bit precision (e2e_bf16 beside an fp16 "
+                         "headline, e2e_fp16 beside a bf16 one; 0 = skip)")
+    ap.add_argument("--cpu-baseline-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--cpu-pin", default="", help=argparse.SUPPRESS)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (0: OMP_NUM_THREADS, else the usable CPUs), pinned one per physical "
+                         "core of one socket")
     return ap.parse_args()
 
 
@@ -150,11 +160,34 @@ def layer_costs(body, h, w, esz=2):
 
 
 def cpu_baseline(args):
-    """Oracle restatement of the reference CPU path, timed on this host."""
+    """Oracle restatement of the reference CPU path, timed on this host in a child
+    process (no GPU in it) pinned before start-up to one CPU per physical core."""
+    import subprocess
+    threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", 0)) or len(os.sched_getaffinity(0))
+    cores = pick_physical_cores(threads)
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-child",
+           "--cpu-pin", ",".join(str(c) for c in cores), "--cpu-threads", str(len(cores) or threads),
+           "--cpu-images", str(args.cpu_images), "--cpu-queries", str(args.cpu_queries),
+           "--cpu-db-rows", str(args.cpu_db_rows), "--db-rows", str(args.db_rows), "--dim", str(args.dim),
+           "--height", str(args.height), "--width", str(args.width), "--arch", args.arch]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=1800)
+    if r.returncode != 0:
+        raise RuntimeError("cpu baseline child failed (rc %d): %s" % (r.returncode, r.stderr[-2000:]))
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def cpu_baseline_child(args):
+    """the timed CPU run (see cpu_baseline); pinned first, before torch's thread pool exists"""
+    cores = [int(c) for c in args.cpu_pin.split(",") if c] if args.cpu_pin else []
+    if cores:
+        try:
+            os.sched_setaffinity(0, cores)
+        except OSError:
+            cores = []
     import numpy as np
     from oracle import backbone as obb, data, weights
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    threads = args.cpu_threads
     torch.set_num_threads(threads)
     net = obb.OracleNet(args.arch, weights.backbone_state(args.arch), weights.head_state(weights.OUTPUT_DIM[args.arch]))
     imgs = torch.from_numpy(data.images(args.cpu_images, args.height, args.width))
@@ -173,16 +206,64 @@ def cpu_baseline(args):
     del ranks, scores, db
     per_img = t_ext + t_match
     model, sockets = host_cpu()
+    per_socket = socket_cores()
     scaled = "" if args.cpu_db_rows == args.db_rows else ", scaled x%.0f to %d rows" % (
         args.db_rows / args.cpu_db_rows, args.db_rows)
     return {"value": 1.0 / per_img, "unit": "images/s", "cores": threads, "kind": "port",
             "host_cpu": model, "sockets": sockets, "logical_cpus": os.cpu_count(),
+            "physical_cores_per_socket": per_socket, "pinned_cpus": cores,
             "extract_s_per_image": t_ext, "match_s_per_query": t_match,
             "sample": ("oracle restatement (torch-CPU conv/BN/leaky + GeM/L2N/whiten) of %d x 3x%dx%d images "
                        "at batch 1 (%.3f s/img) + the reference match np.dot + np.argsort(-scores, axis=0) of %d "
-                       "queries against a %d x %d float32 DB%s (%.3f s/query); host %s, %d socket(s), %d threads used"
+                       "queries against a %d x %d float32 DB%s (%.3f s/query); host %s, %d socket(s) of %s physical "
+                       "cores; %d threads used, pinned one per physical core of socket 0 (%s) -- the GPU box's CPU "
+                       "share per GPU is 16 (OMP_NUM_THREADS), so a full socket is not available to this run"
                        % (args.cpu_images, args.height, args.width, t_ext, args.cpu_queries, args.cpu_db_rows, args.dim,
-                          scaled, t_match, model, sockets, threads))}
+                          scaled, t_match, model, sockets, per_socket, threads,
+                          "pinned" if cores else "not pinned: affinity unavailable"))}
+
+
+def _cpu_topology():
+    """{cpu: (socket, core)} of the CPUs this process may run on (sysfs)"""
+    topo = {}
+    for cpu in sorted(os.sched_getaffinity(0)):
+        base = "/sys/devices/system/cpu/cpu%d/topology/" % cpu
+        try:
+            topo[cpu] = (int(open(base + "physical_package_id").read()), int(open(base + "core_id").read()))
+        except (OSError, ValueError):
+            return {}
+    return topo
+
+
+def socket_cores():
+    """physical cores per socket of this host (all CPUs, not only the usable ones)"""
+    cores = set()
+    try:
+        for d in os.listdir("/sys/devices/system/cpu"):
+            if d.startswith("cpu") and d[3:].isdigit():
+                base = "/sys/devices/system/cpu/%s/topology/" % d
+                cores.add((int(open(base + "physical_package_id").read()), int(open(base + "core_id").read())))
+    except (OSError, ValueError):
+        return None
+    socks = {s for s, _ in cores}
+    return len(cores) // max(1, len(socks)) if cores else None
+
+
+def pick_physical_cores(n):
+    """n usable CPUs on distinct physical cores (no SMT siblings), from the socket with
+    the most usable cores first; [] if the topology is unavailable"""
+    topo = _cpu_topology()
+    if not topo:
+        return []
+    by_sock = {}
+    for cpu, (sk, core) in topo.items():
+        by_sock.setdefault(sk, {}).setdefault(core, cpu)
+    picked = []
+    for sk in sorted(by_sock, key=lambda k: -len(by_sock[k])):
+        picked += sorted(by_sock[sk].values())
+        if len(picked) >= n:
+            break
+    return picked[:n]
 
 
 def host_cpu():
@@ -528,16 +609,26 @@ def bench_dropin(net, H, W, dev, n_files=128, distinct=16):
 
 def main():
     args = parse()
+    if args.cpu_baseline_child:      # the CPU baseline's own process: no GPU here
+        print(json.dumps(cpu_baseline_child(args)))
+        return
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = 0 if args.one_device else int(os.environ.get("LOCAL_RANK", 0))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group("gloo")
+        import datetime
+        try:
+            if args.dist_backend == "nccl":   # RCCL over xGMI
+                dist.init_process_group("nccl", device_id=dev, timeout=datetime.timedelta(minutes=10))
+            else:
+                dist.init_process_group("gloo", timeout=datetime.timedelta(minutes=10))
+            dist.barrier()                    # the communicator is really up before anything is timed
+        except Exception as e:                # noqa: BLE001 -- any init failure ends the run, loudly
+            print("bench.py: rank %d/%d: %s process-group init failed: %s: %s"
+                  % (rank, world, args.dist_backend, type(e).__name__, e), file=sys.stderr, flush=True)
+            sys.exit(3)
 
     def max_over_ranks(x):
         """max of a host float over the ranks (RCCL: a device tensor; gloo: a host one)"""
@@ -638,44 +729,51 @@ def main():
         elapsed = max_over_ranks(time.perf_counter() - t0)
         body_ms = sum(a.elapsed_time(b) for a, b in ev_pairs) / args.steps   # extractor time per step
 
-        # the same step with fp16 operands / activations and an fp16-screened
-        # index: the precision that meets the north_star descriptor bar
-        e2e_fp16 = None
-        if args.fp16_steps > 0 and args.precision == "bf16":
-            net16 = make_net(args.arch, precision="fp16", mean=[0.485, 0.456, 0.406], std=[0.229, 0.224, 0.225])
-            random_init_(net16, seed=0)
-            net16 = net16.to(dev).eval()
-            index16 = ShardedIndex(db32, r0, precision="fp16")
+        # the same step in the other 16-bit precision (bf16 = BASELINE config 2 beside
+        # the fp16 headline, which meets the north_star descriptor bar)
+        e2e_alt, alt = None, {"fp16": "bf16", "bf16": "fp16"}.get(args.precision)
+        if args.alt_steps > 0 and alt is not None:
+            net_a = make_net(args.arch, precision=alt, mean=[0.485, 0.456, 0.406], std=[0.229, 0.224, 0.225])
+            random_init_(net_a, seed=0)
+            net_a = net_a.to(dev).eval()
+            index_a = ShardedIndex(db32, r0, precision=alt)
             saved = (state["net"], state["index"])
-            state["net"], state["index"] = net16, index16
-            for _ in range(2):
+            state["net"], state["index"] = net_a, index_a
+            for _ in range(max(2, args.warmup)):
                 step(False)
             torch.cuda.synchronize()
             if world > 1:
                 dist.barrier()
-            t16 = time.perf_counter()
-            for _ in range(args.fp16_steps):
+            ta = time.perf_counter()
+            for _ in range(args.alt_steps):
                 step(False)
             torch.cuda.synchronize()
             if world > 1:
                 dist.barrier()
-            el16 = max_over_ranks(time.perf_counter() - t16)
+            el_a = max_over_ranks(time.perf_counter() - ta)
             state["net"], state["index"] = saved
-            e2e_fp16 = {"value": world * B * args.fp16_steps / el16, "unit": "images/s",
-                        "ms_per_step": el16 / args.fp16_steps * 1e3, "steps": args.fp16_steps,
-                        "note": "the headline step (extract B images + top-k search of all queries vs the sharded "
-                                "1M DB) with fp16 operands/activations and an fp16 screening copy; descriptor "
-                                "cosine vs the reference: precisions.fp16"}
-            del net16, index16
+            e2e_alt = {"value": world * B * args.alt_steps / el_a, "unit": "images/s", "dtype": alt,
+                       "ms_per_step": el_a / args.alt_steps * 1e3, "steps": args.alt_steps,
+                       "note": "the headline step (extract B images + top-k search of all queries vs the sharded "
+                               "1M DB) with %s operands/activations and a %s screening copy; descriptor cosine vs "
+                               "the reference: precisions.%s" % (alt, alt, alt)}
+            del net_a, index_a
             torch.cuda.empty_cache()
 
-        # extract-only loop (same net, no matching)
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        for _ in range(max(3, args.steps // 2)):
+        # extract-only loop (same net, no matching); warm-up first: the model swap and
+        # empty_cache above returned the activation buffers, which must not be
+        # re-allocated inside the timed loop
+        n_ext = max(3, args.steps // 2)
+        for _ in range(max(2, args.warmup)):
             extract_all(False)
         torch.cuda.synchronize()
-        ext_only = max(3, args.steps // 2) * B / max_over_ranks(time.perf_counter() - t1)
+        if world > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+        for _ in range(n_ext):
+            extract_all(False)
+        torch.cuda.synchronize()
+        ext_only = n_ext * B / max_over_ranks(time.perf_counter() - t1)
 
         # PCIe-inclusive extraction (not `value`: the timed step starts with the
         # images resident in HBM): the step's B images from pinned host memory,
@@ -784,6 +882,35 @@ def main():
                     % (os.path.relpath(kpath, REPO), kc.get("source_commit", "?"),
                        "" if kfresh else "; STALE (kernel sources changed since: digest %s vs %s), not attached"
                        % (kc.get("source_digest", "?"), kernel_source_digest())))
+
+        # the step's two collectives on their own (N > 1): the query all-gather
+        # (B x D fp32 per rank) and the per-shard top-k exchange (one all-gather of
+        # the packed (score, index) lists + the merge), HIP events on this stream
+        comm = None
+        if world > 1:
+            qd = torch.randn((B, args.dim), generator=g, device=dev)
+            sl, il = index.local.search(all_gather_stacked(qd).reshape(world * B, args.dim), args.k)
+            ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            res = {}
+            for name, fn in (("query_allgather", lambda: all_gather_stacked(qd)),
+                             ("topk_allgather_merge", lambda: index.exchange(sl, il, args.k))):
+                for _ in range(3):
+                    fn()
+                torch.cuda.synchronize()
+                dist.barrier()
+                ea.record()
+                for _ in range(20):
+                    fn()
+                eb.record()
+                torch.cuda.synchronize()
+                res[name] = max_over_ranks(ea.elapsed_time(eb) / 20)
+            comm = {"query_allgather_ms": res["query_allgather"],
+                    "topk_allgather_merge_ms": res["topk_allgather_merge"],
+                    "query_bytes_per_rank": B * args.dim * 4, "topk_bytes_per_rank": world * B * args.k * 16,
+                    "share_of_step": (res["query_allgather"] + res["topk_allgather_merge"]) / (elapsed / args.steps * 1e3),
+                    "backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                    "note": "max over ranks of the mean of 20 back-to-back calls (HIP events); in the step the "
+                            "two collectives run on the search stream beside the next extraction"}
 
     traffic, traffic_note = None, "no PMC traffic file for this config"
     t, tpath, tfresh = pmc_file("traffic", lambda c: (c.get("arch"), c.get("precision"), c.get("image")) == (
@@ -901,7 +1028,8 @@ def main():
         "dist": {"world_size": dist.get_world_size() if dist.is_initialized() else 1,
                  "backend": dist.get_backend() if dist.is_initialized() else None,
                  "note": "backend nccl = RCCL over xGMI on ROCm"},
-        "e2e_fp16": e2e_fp16,
+        "e2e_%s" % alt if alt else "e2e_alt": e2e_alt,
+        "comm": comm,
         "knn": knn,
         "local": local,
         "latency": latency,

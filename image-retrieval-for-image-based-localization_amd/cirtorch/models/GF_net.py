@@ -311,7 +311,7 @@ def _default_workers():
 
 
 def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], msp=1, print_freq=10,
-                    batch=64, workers=None, test_transform=None):
+                    batch=64, workers=None, test_transform=None, _no_procs=False):
     """Upstream ``extract_vectors`` (``scripts/test.py:200,236-238``): returns a
     CPU float32 tensor D x len(images).  ``images`` are file paths (PIL load,
     bbx crop, longest side resized to image_size — or ``test_transform``, an
@@ -431,12 +431,15 @@ def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], 
     # shared-memory ring (cirtorch/utils/decode_procs.py); RR_DECODE_PROCS=0: threads.
     procs = None
     if (pinned_files and workers > 1 and n >= 2 * batch and os.environ.get("RR_DECODE_PROCS", "1") != "0"
-            and all(isinstance(it, str) for it in images)):
+            and not _no_procs and all(isinstance(it, str) for it in images)):
         from ..utils import decode_procs
-        ahead = max(2, 2 * batch)   # 2 chains in decode keep every worker busy
         # slots: pending decodes + decoded images waiting in size groups (each <= ahead)
-        # + the chains whose H2D copy is in flight (<= 2 x batch)
-        procs = decode_procs.get(workers, 2 * ahead + 2 * batch + 8)
+        # + the chains whose H2D copy is in flight (<= 2 x batch); ahead = 2 chains in
+        # decode keep every worker busy.  None (no room in /dev/shm, no page-locking):
+        # the decode threads below.
+        procs = decode_procs.get(workers, 6 * batch + 8, decode_procs.slot_bytes_for(image_size))
+        if procs is not None:
+            ahead = max(2, 2 * batch)
 
     first1 = workers if os.environ.get("RR_EV_FIRST1", "0") == "1" else 0  # single-file first tasks (A/B knob)
 
@@ -497,6 +500,21 @@ def extract_vectors(net, images, image_size, transform=None, bbxs=None, ms=[1], 
             if outs:
                 cols = torch.tensor([c for part, _ in outs for c in part], dtype=torch.long).to(dev)
                 vecs[:, cols] = torch.cat([v for _, v in outs], dim=1)
+    except Exception as e:
+        if procs is None:
+            raise
+        # the process decoder's slots held by undelivered images are lost with the
+        # error: drop the cached decoder (a later call builds a fresh ring)
+        from ..utils import decode_procs
+        decode_procs.drop()
+        if not isinstance(e, decode_procs.DecoderFailure):
+            raise
+        import warnings
+        warnings.warn("extract_vectors: the process decoder failed (%s); decoding on threads instead" % e)
+        net.augment = saved
+        return extract_vectors(net, images, image_size, transform=transform, bbxs=bbxs, ms=ms, msp=msp,
+                               print_freq=print_freq, batch=batch, workers=workers, test_transform=test_transform,
+                               _no_procs=True)
     finally:
         net.augment = saved
     out = vecs.cpu()

@@ -143,6 +143,7 @@ def knn(vecs, qvecs, k, precision="fp32", cand=0):
     return i.t(), s.t()
 
 
+RANK_BYTES_MAX = 2 << 30  # device scratch + output of one rr_rank_full call
 RANK_KNN_MAX = 8192  # up to this size the top-k pipeline (LDS bitonic sort of all rows) ranks in one pass
 
 
@@ -157,7 +158,16 @@ def rank(vecs, qvecs, precision="fp32", method="auto"):
         return ranks
     db, q = _rows(vecs), _rows(qvecs)
     d_pad = (db.shape[1] + 255) // 256 * 256
-    return _ops.rank_full(_pad_cols(db, d_pad), _pad_cols(q, d_pad)).t()
+    db, q = _pad_cols(db, d_pad), _pad_cols(q, d_pad)
+    # ~32 B of scratch + output per (query, row): queries in independent groups that
+    # fit RANK_BYTES_MAX (and the kernels' 65535-query grid), each ranked on its own
+    per = max(1, min(65535, RANK_BYTES_MAX // (32 * n)))
+    if q.shape[0] <= per:
+        return _ops.rank_full(db, q).t()
+    out = torch.empty((n, q.shape[0]), dtype=torch.int64, device=db.device)
+    for j in range(0, q.shape[0], per):
+        out[:, j:j + per] = _ops.rank_full(db, q[j:j + per].contiguous()).t()
+    return out
 
 
 def shard_range(n, rank, world):
@@ -188,7 +198,7 @@ class ShardedIndex:
     first if each rank extracted its own).
 
     The only exchange is one all-gather of the per-shard (score f64, index i64)
-    lists — Q x k x 16 bytes per rank — followed by the on-GPU merge with the
+    lists, packed in one buffer — Q x k x 16 bytes per rank — followed by the on-GPU merge with the
     (score desc, index asc) rule, so the merged result is bit-identical to a
     single-GPU search of the whole database."""
 
@@ -202,7 +212,14 @@ class ShardedIndex:
         s, i = self.local.search(q_rows, k)
         if self.world == 1:
             return s, i
-        return self.merge(all_gather_stacked(s, self.group), all_gather_stacked(i, self.group), k)
+        return self.exchange(s, i, k)
+
+    def exchange(self, s, i, k):
+        """per-shard (score f64, index i64) [Q, k] -> merged [Q, k]: ONE all-gather of
+        the two lists packed as int64 pairs [Q, k, 2] (16 B per entry), then the merge"""
+        packed = torch.stack([s.contiguous().view(torch.int64), i], dim=-1)
+        g = all_gather_stacked(packed, self.group)                 # [R, Q, k, 2]
+        return self.merge(g[..., 0].contiguous().view(torch.float64), g[..., 1].contiguous(), k)
 
 
 def merge_topk(scores, idx, k):

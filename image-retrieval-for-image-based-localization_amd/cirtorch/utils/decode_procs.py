@@ -16,9 +16,15 @@ Host-side plumbing only: the pixels are the same bytes the thread path
 produces (``GF_net._load_pil``), so descriptors are identical.
 """
 
+import os
 import threading
 
 import numpy as np
+
+
+class DecoderFailure(RuntimeError):
+    """the process decoder itself failed (a worker died, e.g. SIGBUS on a full
+    /dev/shm): extract_vectors falls back to its decode threads"""
 
 _SHM = None  # worker side: the parent's ring
 
@@ -70,7 +76,15 @@ class _Pending:
 
     def result(self):
         import torch
-        out = self.res.get(timeout=300)
+        # wait in slices: a worker that died (its task is lost for good) is noticed
+        # within a second instead of at the timeout
+        for _ in range(300):
+            if self.res.ready():
+                break
+            self.res.wait(1.0)
+            if not self.res.ready() and self.owner.worker_died():
+                raise DecoderFailure("a decode worker process died")
+        out = self.res.get(timeout=1.0)
         shape, big = out if self.k is None else out[self.k]
         if big is not None:
             self.owner._give_back([self.slot])
@@ -111,10 +125,16 @@ class ProcDecoder:
             self.pool = mp.get_context("spawn").Pool(workers, initializer=_worker_init, initargs=(self.shm.name,))
         finally:
             sys.modules["__main__"] = main
+        self._procs = list(getattr(self.pool, "_pool", []))  # the workers as started
         self.lock = threading.Lock()
         self.free = list(range(nslots))
         self.busy = []      # (event, [slots]) waiting for their H2D copy
         self.slot_of = {}   # data_ptr of a handed-out view -> slot
+
+    def worker_died(self):
+        """True once any of the started workers has exited (multiprocessing.Pool
+        replaces a dead worker but never re-runs the task it held)"""
+        return any(p.exitcode is not None for p in self._procs)
 
     def _reclaim(self, block):
         keep = []
@@ -190,17 +210,56 @@ class ProcDecoder:
 
 _DEC = {}
 
+RING_MAX_BYTES = 2 << 30   # never more than 2 GiB of /dev/shm
+SHM_SHARE = 0.5            # nor more than half of what /dev/shm has free
 
-def get(workers, nslots):
-    """the process decoder of this host process (created on first use, kept: the
-    workers' start-up is paid once); re-created if asked for more workers / slots"""
-    import atexit
-    d = _DEC.get("d")
-    if d is not None and d.workers >= workers and d.nslots >= nslots:
-        return d
+
+def slot_bytes_for(image_size):
+    """ring slot size: one decoded RGB image of at most image_size x image_size
+    (thumbnail), or a 1024 x 1024 one when the size is not capped; larger images
+    come back pickled instead"""
+    side = int(image_size) if image_size else 1024
+    return max(64 << 10, (side * side * 3 + 4095) // 4096 * 4096)
+
+
+def shm_free_bytes(path="/dev/shm"):
+    try:
+        st = os.statvfs(path)
+        return st.f_bavail * st.f_frsize
+    except OSError:
+        return 0
+
+
+def drop():
+    """close and forget the cached decoder (after an error: its slots may be held
+    by deliveries that will never happen)"""
+    d = _DEC.pop("d", None)
     if d is not None:
         d.close()
-    d = _DEC["d"] = ProcDecoder(workers, nslots)
+
+
+def get(workers, nslots, slot_bytes=3 << 20):
+    """the process decoder of this host process (created on first use, kept: the
+    workers' start-up is paid once); re-created if asked for more workers / slots /
+    larger slots.  None when the ring does not fit (RING_MAX_BYTES, or SHM_SHARE of
+    the free /dev/shm: a worker writing past a full tmpfs dies of SIGBUS) or cannot
+    be page-locked: the caller decodes on threads instead."""
+    import atexit
+    d = _DEC.get("d")
+    if d is not None and d.workers >= workers and d.nslots >= nslots and d.slot_bytes >= slot_bytes:
+        return d
+    drop()
+    need = nslots * slot_bytes
+    if need > RING_MAX_BYTES or need > SHM_SHARE * shm_free_bytes():
+        return None
+    try:
+        d = ProcDecoder(workers, nslots, slot_bytes)
+    except (OSError, ValueError, RuntimeError):
+        return None
+    if not d.registered:
+        d.close()
+        return None
+    _DEC["d"] = d
     if not _DEC.get("atexit"):
         atexit.register(lambda: _DEC["d"].close() if _DEC.get("d") else None)
         _DEC["atexit"] = True

@@ -66,8 +66,9 @@ def pre_train_from_snapshots(model, snapshots, modules):
             if module_name not in modules:
                 raise ValueError("Unrecognized network module {}".format(module_name))
             sd = _module_state(state_dict, module_name)
-            if sd is not None:
-                _load_pretraining_dict(getattr(model, module_name), sd)
+            if sd is None:  # an explicitly named module must be in the file (reference snapshot.py:35-36)
+                raise KeyError("The given snapshot does not contain a state_dict for module '{}'".format(module_name))
+            _load_pretraining_dict(getattr(model, module_name), sd)
 
 
 def resume_from_snapshot(model, snapshot, modules):

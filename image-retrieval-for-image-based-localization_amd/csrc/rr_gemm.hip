@@ -649,6 +649,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int n
     const bool tau_lds = !PERM && sizeof(TO) == 4 && a.scr_k && a.P <= 1024;
     if (tau_lds) {
         for (int q = tid; q < a.P; q += 512) lds_tau[q] = a.scr_tau[q];
+        __syncthreads();  // visible to every wave before any epilogue reads it
     }
     const int wn = wave & 3;                // 32-column quarter of each quadrant
     // XCD-contiguous bijective tile order (blocks are dispatched round-robin over 8 XCDs)
@@ -1233,6 +1234,9 @@ __global__ void __launch_bounds__(512, 1) k_gemm8s(ConvArgs a, int ntiles) {
     uint32_t* const lds_stage = lds_tau + 128;
     if (a.scr_k) {
         for (int q = tid; q < a.P; q += 512) lds_tau[q] = a.scr_tau[q];
+        // visible to every wave before any epilogue reads it: with one K-step per
+        // tile (D = 64) the first epilogue comes before a second block barrier
+        __syncthreads();
     }
     // issue side: stream position (mi, ki); this lane's two DB rows of tile mi
     // (positions past the block's stream re-read its last tile: same count of
@@ -1340,10 +1344,6 @@ __global__ void __launch_bounds__(512, 1) k_gemm8s(ConvArgs a, int ntiles) {
 #pragma unroll
                         for (int r = 0; r < 4; ++r) v[r] = acc[g][j][r];
                         acc[g][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-                        if (a.scr_k) {
-                            screen_append(a, v, c, a.cout, p, a.scr_tau[p]);
-                            continue;
-                        }
                         const long long o = (long long)p * a.ldy + c;
                         if (full) {
                             St4<float>::st(Y + o, v);

@@ -220,6 +220,7 @@ int rr_rank_full(const float* db_f32, long long n, const float* q_f32, int nq, i
     if ((size_t)RQG * d * 4 > 160 * 1024) return fail(RR_EINVAL, "rr_rank_full: d too large for the LDS query tile");
     const RankPlan p = rank_plan(n, nq);
     if (!workspace || workspace_bytes < p.total) return fail(RR_ENOSPACE, "rr_rank_full: workspace too small");
+    if (nq > 65535) return fail(RR_EINVAL, "rr_rank_full: more than 65535 queries per call (grid y); split them");
     if ((long long)nq * p.ntiles > 0x7fffffffll)
         return fail(RR_EINVAL, "rr_rank_full: problem too large");
     hipStream_t s = as_stream(stream);

@@ -217,3 +217,22 @@ def nn_matcher(desc1, desc2):
     n1 = n1.copy()
     n1[n2[n1] != np.arange(len(n1))] = -1
     return n1
+
+
+# ---------------------------------------------------------------- upstream multi-scale rule
+def extract_ms_upstream(net, x, ms, msp, whiten):
+    """One image through the upstream ``extract_vectors(ms, msp)`` rule that
+    ``scripts/test.py:200,236-238`` calls: for every scale s the image (already
+    normalised, C x H x W) is bilinearly resized (align_corners=False; s = 1 ->
+    as is), its descriptor f_s is raised to msp, the mean over scales is taken to
+    the power 1 / msp and the result is L2-normalised.  The upstream source
+    (cirtorch/networks/imageretrievalnet.py of cnnimageretrieval-pytorch) is not
+    in /root/reference: PARITY UNPINNED for this rule (restated from its
+    published description).  net: an oracle.backbone.OracleNet; returns D."""
+    acc = None
+    for s in ms:
+        xs = x[None] if s == 1 else F.interpolate(x[None], scale_factor=s, mode="bilinear", align_corners=False)
+        v = net.head(net.body(xs)["mod5"], whiten=whiten)[:, 0].pow(msp)
+        acc = v if acc is None else acc + v
+    v = (acc / len(ms)).pow(1.0 / msp)
+    return v / v.norm()

@@ -264,6 +264,94 @@ def gen_mixed(arch, sizes, seed, fname):
     np.savez_compressed(os.path.join(HERE, fname), **out)
 
 
+# ----------------------------------------------------------------------------- G10
+def gen_testpy():
+    """scripts/test.py:84-259 replayed (tests/testpy_replay.py) with the oracle
+    extractor (torch-CPU restatement, decoded by the same PIL calls) and the
+    reference's own whitenlearn / whitenapply / compute_map_and_print.  The upstream
+    multi-scale power mean of extract_vectors (msp) is not in /root/reference
+    (parity unpinned for that rule: restated as oracle.ops.extract_ms_upstream).
+    Two cases: (A) meta whitening=False -> msp = pool.p = 3; (B) whitening=True
+    (head Linear with the centering bias) -> msp = 1.  Each is also run with a
+    float64 oracle; the stored ranks are required to be the same in both, so a
+    float32 engine cannot differ from them by rounding alone."""
+    import tempfile
+    import types as _types
+    from PIL import Image
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import testpy_replay as T
+    out = {}
+    with tempfile.TemporaryDirectory() as root:
+        hashes = T.make_dataset(root)
+        names = sorted(hashes)
+        out["file_names"] = np.array(names)
+        out["file_sha1"] = np.array([hashes[k] for k in names])
+        bias = centering_bias(T.ARCH)
+        out["head_bias"] = bias
+        for tag, whitening in (("A", False), ("B", True)):
+            ck = os.path.join(root, "ck_%s.pth" % tag)
+            T.checkpoint(ck, whitening, bias if whitening else None)
+            runs = {}
+            for dt in (torch.float32, torch.float64):
+                def load_net(state, dt=dt):
+                    meta = state["meta"]
+                    sd = state["state_dict"]
+                    bs = {k[5:]: v.numpy() for k, v in sd.items() if k.startswith("body.")}
+                    hs = {k[9:]: v.numpy() for k, v in sd.items() if k.startswith("ret_head.")}
+                    net = obb.OracleNet(meta["architecture"], bs, hs, dtype=dt)
+                    return (net, meta["whitening"]), meta, float(hs["pool.p"].reshape(-1)[0])
+
+                def extract(netw, images, size, bbxs, ms, msp, dt=dt):
+                    net, whiten = netw
+                    cols = []
+                    for i, p in enumerate(images):
+                        with open(p, "rb") as f:
+                            img = Image.open(f).convert("RGB")
+                        if bbxs is not None:
+                            img = img.crop(bbxs[i])
+                        img.thumbnail((size, size), Image.LANCZOS)
+                        x = torch.from_numpy(np.asarray(img, dtype=np.float32).transpose(2, 0, 1).copy() / 255.0)
+                        x = obb.normalize_images(x.to(dt), T.MEAN, T.STD)
+                        cols.append(ops.extract_ms_upstream(net, x, ms, msp, whiten))
+                    return torch.stack(cols, 1)
+
+                api = _types.SimpleNamespace(
+                    load_net=load_net, extract_vectors=extract,
+                    whitenlearn=lambda X, q, p_: R_whiten.whitenlearn(X, q, p_),
+                    whitenapply=lambda X, m, P: R_whiten.whitenapply(X, m, P),
+                    compute_map=lambda ds, ranks, gnd: R_eval.compute_map_and_print(ds, ranks, gnd, lambda *a: None),
+                    cid2filename=lambda cid, prefix: os.path.join(prefix, cid[-2:], cid[-4:-2], cid[-6:-4], cid),
+                    configdataset=_oracle_configdataset,
+                    to_numpy=lambda v: v.float().numpy())
+                with torch.no_grad():
+                    runs[dt] = T.run(api, root, ck)
+            r32, r64 = runs[torch.float32], runs[torch.float64]
+            for key in ("ranks", "ranks_lw"):
+                same = (r32[key] == r64[key]).all()
+                diff = np.argwhere(r32[key] != r64[key])
+                print("  testpy %s %s: float32 == float64 oracle ranks: %s (%d entries differ: %s)"
+                      % (tag, key, same, len(diff), diff[:10].tolist()))
+                out["%s_%s_stable" % (tag, key)] = np.bool_(same)
+            print("  testpy %s: msp %g, mAP %.4f, + whiten %.4f" % (tag, r32["msp"], r32["map"]["mAP"],
+                                                                   r32["map_lw"]["mAP"]))
+            out.update({tag + "_ranks": r32["ranks"].astype(np.int32), tag + "_ranks_lw": r32["ranks_lw"].astype(np.int32),
+                        tag + "_map": np.float64(r32["map"]["mAP"]), tag + "_map_lw": np.float64(r32["map_lw"]["mAP"]),
+                        tag + "_vecs": r32["vecs"], tag + "_qvecs": r32["qvecs"], tag + "_msp": np.float64(r32["msp"])})
+    np.savez_compressed(os.path.join(HERE, "testpy.npz"), **out)
+
+
+def _oracle_configdataset(dataset, dir_main):
+    """upstream configdataset (the gnd pickle is this script's own file)"""
+    import pickle
+    with open(os.path.join(dir_main, dataset, "gnd_%s.pkl" % dataset), "rb") as f:
+        cfg = pickle.load(f)
+    cfg["n"], cfg["nq"] = len(cfg["imlist"]), len(cfg["qimlist"])
+    d = os.path.join(dir_main, dataset, "jpg")
+    cfg["im_fname"] = lambda c, i: os.path.join(d, c["imlist"][i] + ".jpg")
+    cfg["qim_fname"] = lambda c, i: os.path.join(d, c["qimlist"][i] + ".jpg")
+    return cfg
+
+
 # ----------------------------------------------------------------------------- G4
 def gen_knn():
     out = {}
@@ -444,6 +532,8 @@ GENERATORS = {
     "r152": lambda: gen_net("resnet152", (768, 1024), 1, 2401, [(1,)], "r152.npz", local=("mod3", 512, 128, 2402)),
     # a2: a ragged R50 batch at 768x1024 / 640x960 / 700x1000 (both pad orders)
     "r50mixed": lambda: gen_mixed("resnet50", [(768, 1024), (640, 960), (700, 1000)], 2501, "r50mixed.npz"),
+    # the scripts/test.py call sequence on a synthetic roxford5k + Lw dataset
+    "testpy": lambda: gen_testpy(),
     "knn": lambda: gen_knn(),
     "map": lambda: gen_map(),
     "whiten": lambda: gen_whiten(),

@@ -9,6 +9,8 @@ image at its own address and pads to the max extent on the fly.  Checked
   * bit for bit against the same engine on the explicitly padded batch
     (ragged and padded runs must be the same computation);
   * rr_pad_images (pad_packed_images on device tensors) against the host path.
+Plus the scripts/test.py:84-259 replay through the product vs the oracle's run
+of the same sequence (tests/testpy_replay.py, tests/golden/testpy.npz).
 """
 
 import numpy as np
@@ -155,3 +157,80 @@ def test_pad_packed_images_device_equals_host(cuda, dtype):
     ph, _ = pad_packed_images(PackedSequence(h2), pad_value=-1.0)
     pd, _ = pad_packed_images(PackedSequence([t.to(cuda) for t in h2]), pad_value=-1.0)
     assert torch.equal(pd.cpu(), ph) and ph.shape == (2, 5, 6)
+
+
+# ------------------------------------------------------------------ scripts/test.py replay
+class _ToTensorNormalize:
+    """transforms.Compose([ToTensor(), Normalize(mean, std)]) of scripts/test.py:149-156
+    (torchvision is absent: to_tensor = HWC uint8 -> CHW float32 / 255, then (x - m) / s)"""
+
+    def __init__(self, mean, std):
+        self.m = torch.tensor(mean)[:, None, None]
+        self.s = torch.tensor(std)[:, None, None]
+
+    def __call__(self, pil):
+        x = torch.from_numpy(np.asarray(pil, dtype=np.float32).transpose(2, 0, 1).copy() / 255.0)
+        return (x - self.m) / self.s
+
+
+def _product_api(precision):
+    import types
+    from cirtorch.datasets.datahelpers import cid2filename
+    from cirtorch.datasets.testdataset import configdataset
+    from cirtorch.models.GF_net import init_network, extract_vectors
+    from cirtorch.utils.evaluate import compute_map_and_print
+    from cirtorch.utils.whiten import whitenlearn, whitenapply
+
+    def load_net(state):
+        meta = state["meta"]
+        params = {"architecture": meta["architecture"], "pooling": meta["pooling"],
+                  "local_whitening": meta.get("local_whitening", False), "regional": meta.get("regional", False),
+                  "whitening": meta.get("whitening", False), "mean": meta["mean"], "std": meta["std"],
+                  "pretrained": False}
+        if precision is not None:
+            params["precision"] = precision
+        net = init_network(params)
+        net.load_state_dict(state["state_dict"])
+        net.cuda()
+        net.eval()
+        return net, net.meta, net.pool.p.item()
+
+    def extract(net, images, size, bbxs, ms, msp):
+        tf = _ToTensorNormalize(net.meta["mean"], net.meta["std"])
+        return extract_vectors(net, images, size, tf, bbxs=bbxs, ms=ms, msp=msp)
+
+    return types.SimpleNamespace(load_net=load_net, extract_vectors=extract, whitenlearn=whitenlearn,
+                                 whitenapply=whitenapply, compute_map=compute_map_and_print,
+                                 cid2filename=cid2filename, configdataset=configdataset,
+                                 to_numpy=lambda v: v.numpy())
+
+
+@pytest.mark.parametrize("case,precision", [("A", "fp32"), ("B", "fp32"), ("B", None)])
+def test_scripts_test_replay(cuda, tmp_path, case, precision):
+    """scripts/test.py:84-259 as one sequence through the product -- checkpoint load,
+    init_network, Lw learned from extract_vectors of a whitening db, configdataset,
+    extract_vectors (ms = [1, 1/sqrt2, sqrt2], msp = pool.p for case A; query bbx
+    crops), np.dot / np.argsort, 3-argument compute_map_and_print, whitenapply,
+    re-rank -- equals the oracle's run of the same sequence (tests/golden/testpy.npz).
+    Case A: meta whitening=False (msp = 3); B: whitening=True (msp = 1), also at the
+    init_network default precision (fp16).  B's Lw re-rank is decided by rounding
+    (the float32 and float64 oracle runs disagree on it), so only its plain rank and
+    mAP are compared."""
+    import testpy_replay as T
+    g = golden("testpy.npz")
+    hashes = T.make_dataset(str(tmp_path))
+    names = sorted(hashes)
+    assert names == [str(x) for x in g["file_names"]]
+    assert [hashes[k] for k in names] == [str(x) for x in g["file_sha1"]], "JPEG encoder output differs"
+    ck = str(tmp_path / "ck.pth")
+    T.checkpoint(ck, case == "B", g["head_bias"] if case == "B" else None)
+    r = T.run(_product_api(precision), str(tmp_path), ck)
+    assert r["msp"] == float(g[case + "_msp"])
+    bar = FP32_COS if precision == "fp32" else FP16_COS
+    assert cosines(r["vecs"], g[case + "_vecs"]).min() >= bar
+    assert cosines(r["qvecs"], g[case + "_qvecs"]).min() >= bar
+    assert (r["ranks"] == g[case + "_ranks"]).all()
+    assert r["map"]["mAP"] == pytest.approx(float(g[case + "_map"]), abs=1e-9)
+    if bool(g[case + "_ranks_lw_stable"]):
+        assert (r["ranks_lw"] == g[case + "_ranks_lw"]).all()
+        assert r["map_lw"]["mAP"] == pytest.approx(float(g[case + "_map_lw"]), abs=1e-9)

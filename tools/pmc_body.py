@@ -27,12 +27,13 @@ def main():
     ap.add_argument("--height", type=int, default=768)
     ap.add_argument("--width", type=int, default=1024)
     ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--precision", default="fp16")
     args = ap.parse_args()
     from cirtorch import _ops
     from cirtorch.models.GF_net import make_net
     from cirtorch.models.init import random_init_
 
-    net = make_net(args.arch, precision="bf16", mean=[0.485, 0.456, 0.406], std=[0.229, 0.224, 0.225])
+    net = make_net(args.arch, precision=args.precision, mean=[0.485, 0.456, 0.406], std=[0.229, 0.224, 0.225])
     random_init_(net, seed=0)
     net = net.cuda().eval()
     x = torch.rand(args.batch, 3, args.height, args.width, device="cuda")

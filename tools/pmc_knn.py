@@ -25,12 +25,13 @@ def main():
     ap.add_argument("--q", type=int, default=1024)
     ap.add_argument("--n", type=int, default=1_000_000)
     ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--precision", default="fp16")
     args = ap.parse_args()
     from cirtorch import _ops
     from cirtorch.search import KnnIndex
     db = _ops.fill_unit_rows(args.n, 2048, seed=0xDB5EED)
     q = _ops.fill_unit_rows(args.q, 2048, seed=0x0E5EED)
-    index = KnnIndex(db, "bf16")
+    index = KnnIndex(db, args.precision)
     marker = torch.zeros(64, device="cuda")
     for _ in range(2):
         index.search(q, 100)
