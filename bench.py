@@ -36,6 +36,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_I8_TOPS = 5000.0       # dense int8 MFMA: v_mfma_i32_16x16x64_i8 at 2x the bf16 rate per clock
 PEAK_F32_TFLOPS = 157.3     # exact-f32 MFMA
 PEAK_HBM_GBS = 8000.0
 METRIC = "images/sec extract + queries/sec 1M-desc kNN, ResNet50-GeM 1024×768"
@@ -55,6 +56,9 @@ def parse():
     ap.add_argument("--precision", default="fp16", choices=["bf16", "fp16", "fp32"],
                     help="headline precision: fp16 meets the north-star descriptor bar (cosine >= 1 - 1e-4 vs the "
                          "reference); bf16 (BASELINE config 2) runs as the e2e_bf16 sub-line")
+    ap.add_argument("--screen", default="int8", choices=["int8", "bf16", "fp16", "fp32"],
+                    help="kNN screening copy of the database (the top-k is the exact float64 re-score of the "
+                         "candidates in every case): int8 = exact int32 dot products of int8-quantised rows")
     ap.add_argument("--db-rows", type=int, default=1_000_000)
     ap.add_argument("--dim", type=int, default=2048)
     ap.add_argument("--k", type=int, default=100)
@@ -658,7 +662,7 @@ def main():
     r0 = rank * per
     n_local = max(0, min(per, args.db_rows - r0))
     db32 = _ops.fill_unit_rows(n_local, args.dim, seed=0xDB5EED, row0=r0, device=dev)
-    index = ShardedIndex(db32, r0, precision=args.precision)
+    index = ShardedIndex(db32, r0, precision=args.screen)
 
     ev_pairs = []
 
@@ -736,7 +740,7 @@ def main():
             net_a = make_net(args.arch, precision=alt, mean=[0.485, 0.456, 0.406], std=[0.229, 0.224, 0.225])
             random_init_(net_a, seed=0)
             net_a = net_a.to(dev).eval()
-            index_a = ShardedIndex(db32, r0, precision=alt)
+            index_a = ShardedIndex(db32, r0, precision=args.screen)
             saved = (state["net"], state["index"])
             state["net"], state["index"] = net_a, index_a
             for _ in range(max(2, args.warmup)):
@@ -755,8 +759,8 @@ def main():
             e2e_alt = {"value": world * B * args.alt_steps / el_a, "unit": "images/s", "dtype": alt,
                        "ms_per_step": el_a / args.alt_steps * 1e3, "steps": args.alt_steps,
                        "note": "the headline step (extract B images + top-k search of all queries vs the sharded "
-                               "1M DB) with %s operands/activations and a %s screening copy; descriptor cosine vs "
-                               "the reference: precisions.%s" % (alt, alt, alt)}
+                               "1M DB, %s screening) with %s operands/activations; descriptor cosine vs the "
+                               "reference: precisions.%s" % (args.screen, alt, alt)}
             del net_a, index_a
             torch.cuda.empty_cache()
 
@@ -845,12 +849,15 @@ def main():
                 dist.barrier()
             tk = max_over_ranks((time.perf_counter() - t2) / args.knn_steps)
             flops = 2.0 * args.knn_q * n_local * args.dim
-            peak = PEAK_F32_TFLOPS if args.precision == "fp32" else PEAK_BF16_TFLOPS
+            peak = {"fp32": PEAK_F32_TFLOPS, "int8": PEAK_I8_TOPS}.get(args.screen, PEAK_BF16_TFLOPS)
             knn = {"queries_per_sec": args.knn_q / tk, "q": args.knn_q, "db_rows": args.db_rows, "k": args.k,
-                   "ms_per_batch": tk * 1e3,
-                   "roofline": {"bound": "mfma", "achieved": flops / tk / 1e12, "peak": peak, "unit": "TFLOP/s",
+                   "ms_per_batch": tk * 1e3, "screen_dtype": args.screen,
+                   "roofline": {"bound": "mfma", "achieved": flops / tk / 1e12, "peak": peak,
+                                "unit": "TOP/s" if args.screen == "int8" else "TFLOP/s",
                                 "frac": flops / tk / 1e12 / peak, "traffic": None,
-                                "note": "per-rank screening GEMM FLOPs 2*Q*n_local*D / whole search time"}}
+                                "note": "per-rank screening GEMM operations 2*Q*n_local*D / whole search time, vs the "
+                                        "dense MFMA peak of the screening dtype; the returned top-k are the exact "
+                                        "float64 re-scores of the candidates"}}
             # the step's own search alone (B x world queries, no extraction beside it):
             # at <= 128 queries the score GEMM streams the screening copy of the DB
             qs1 = _ops.fill_unit_rows(B * world, args.dim, seed=0x0E5EED + 1, row0=0, device=dev)
@@ -865,14 +872,29 @@ def main():
             if world > 1:
                 dist.barrier()
             ts = max_over_ranks((time.perf_counter() - t3) / args.knn_steps)
-            db_bytes = float(n_local) * args.dim * (4 if args.precision == "fp32" else 2)
+            db_bytes = float(n_local) * args.dim * {"fp32": 4, "int8": 1}.get(args.screen, 2)
             knn["step_search"] = {"q": B * world, "ms_per_search": ts * 1e3, "queries_per_sec": B * world / ts,
                                   "roofline": {"bound": "hbm", "achieved": db_bytes / ts / 1e9, "peak": PEAK_HBM_GBS,
                                                "unit": "GB/s", "frac": db_bytes / ts / 1e9 / PEAK_HBM_GBS,
                                                "note": "screening-copy DB bytes per rank / whole search time"}}
+            # the same Q = knn_q search with a bf16 screening copy (the round-3 pipeline), for comparison
+            if args.screen != "bf16" and world == 1:
+                from cirtorch.search import KnnIndex
+                ib = KnnIndex(db32, "bf16")
+                ib.search(qk, args.k)
+                torch.cuda.synchronize()
+                t4 = time.perf_counter()
+                for _ in range(args.knn_steps):
+                    ib.search(qk, args.k)
+                torch.cuda.synchronize()
+                tb = (time.perf_counter() - t4) / args.knn_steps
+                knn["bf16_screen"] = {"ms_per_batch": tb * 1e3, "queries_per_sec": args.knn_q / tb,
+                                      "same_topk": bool(torch.equal(ib.search(qk, args.k)[1], index.search(qk, args.k)[1]))}
+                del ib
+                torch.cuda.empty_cache()
             kt, kpath, kfresh = pmc_file("knn_q%d" % args.knn_q, lambda c: (
                 c.get("db_rows"), c.get("dim"), c.get("k"), c.get("screen")) == (
-                args.db_rows, args.dim, args.k, args.precision))
+                args.db_rows, args.dim, args.k, args.screen))
             if kt is not None and world == 1:
                 kc = kt.get("config", {})
                 if kfresh:
@@ -1002,9 +1024,10 @@ def main():
         "dtype": args.precision,
         "data": "synthetic (U[0,1) images, random-init weights, counter-hash N(0,1) unit DB rows)",
         "config": {"workload": "%s-GeM+whiten %s extract %dx%d, B=%d/GPU (chains of %d), then top-%d cosine kNN of "
-                               "all %d queries vs %d x %d DB sharded over %d GPU(s)%s"
+                               "all %d queries vs %d x %d DB sharded over %d GPU(s) (%s screening, exact float64 "
+                               "re-score)%s"
                                % (args.arch, args.precision, W, H, B, EB, args.k, B * world, args.db_rows, args.dim,
-                                  world, "; each step's search on a second stream beside the next step's extraction"
+                                  world, args.screen, "; each step's search on a second stream beside the next step's extraction"
                                   if args.overlap else ""),
                    "global_batch": B * world, "extract_batch": EB, "image": [3, H, W], "db_rows": args.db_rows,
                    "dim": args.dim,

@@ -17,13 +17,14 @@ import torch
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("RR_LIB", os.path.join(PKG_DIR, "librr.so"))
 
-RR_F32, RR_BF16, RR_F16 = 0, 1, 2
+RR_F32, RR_BF16, RR_F16, RR_I8 = 0, 1, 2, 3
 RR_ACT_IDENTITY, RR_ACT_LEAKY = 0, 1
 RR_POOL_GEM, RR_POOL_MAC, RR_POOL_SPOC = 0, 1, 2
 RR_CONV_AFFINE, RR_CONV_RESIDUAL, RR_CONV_PERM32 = 1, 2, 4
 RR_NHWC, RR_NCHW = 0, 1
 
-_DTYPE_CODE = {torch.float32: RR_F32, torch.bfloat16: RR_BF16, torch.float16: RR_F16}  # RR_F16: kNN screening only
+_DTYPE_CODE = {torch.float32: RR_F32, torch.bfloat16: RR_BF16, torch.float16: RR_F16,
+               torch.int8: RR_I8}  # RR_I8: kNN screening only
 
 
 class ConvDesc(ctypes.Structure):
@@ -80,6 +81,7 @@ _SIGS = {
     "rr_fill_unit_rows": ([_vp, _ll, _i, ctypes.c_ulonglong, _ll, _vp], _i),
     "rr_cast_f32_bf16": ([_vp, _vp, _ll, _vp], _i),
     "rr_cast_f32_f16": ([_vp, _vp, _ll, _vp], _i),
+    "rr_quantize_i8": ([_vp, _ll, _vp, _vp, _vp], _i),
 }
 
 _lib = None

@@ -120,11 +120,12 @@ def maxpool2d(x, k=3, stride=2, pad=1):
 
 
 def pack_stem_weights(weight, dtype=torch.bfloat16):
-    """conv1 weight [64, 3, 7, 7] (GPU) -> the fused stem's [64, 256] layout (bf16 or fp16)."""
+    """conv1 weight [64, 3, 7, 7] (GPU) -> the fused stem's [64, 448] layout (bf16 or fp16):
+    kernel-row K (v1-v3 stems) then space-to-depth K (v4)."""
     E.require_gpu(weight)
     w = weight.detach().float().contiguous()
     co, ci, kh, kw = w.shape
-    out = torch.empty((co, 256), dtype=dtype, device=w.device)
+    out = torch.empty((co, 448), dtype=dtype, device=w.device)
     E.check(E.lib().rr_stem_pack_weights(E.ptr(w), co, ci, kh, kw, E.ptr(out), E.dtype_code(dtype), _st()),
             "rr_stem_pack_weights")
     return out
@@ -466,10 +467,25 @@ def cast_f16(x):
     return y
 
 
+def quantize_i8(x):
+    """float32 rows -> int8 screening copy: rint(x * 127 / max|x|) clamped to +-127 (one
+    scale for the whole tensor, reduced on the device: no host read-back)."""
+    E.require_gpu(x)
+    x = x.contiguous()
+    y = torch.empty(x.shape, dtype=torch.int8, device=x.device)
+    if x.numel() % 4:
+        raise RuntimeError("quantize_i8: element count must be a multiple of 4")
+    amax = torch.empty(1, dtype=torch.float32, device=x.device)
+    E.check(E.lib().rr_quantize_i8(E.ptr(x), x.numel(), E.ptr(y), E.ptr(amax), _st()), "rr_quantize_i8")
+    return y
+
+
 def cast_screen(x, dtype):
     """float32 rows -> the screening dtype's copy (the rows themselves for float32)."""
     if dtype == torch.float32:
         return x
+    if dtype == torch.int8:
+        return quantize_i8(x)
     if dtype == torch.bfloat16:
         return cast_bf16(x)
     if dtype == torch.float16:

@@ -21,8 +21,12 @@ import torch.distributed as dist
 
 from . import _ops
 
+# screening precision of the score GEMM (the final top-k is always the exact float64
+# re-score): int8 = rows quantised with one scale per tensor, exact int32 dot products
+# on v_mfma_i32_16x16x64_i8 (twice the bf16 rate, half the bytes); no certificate
+# (verify=True re-searches every query in float32)
 _PREC = {"fp32": torch.float32, "float32": torch.float32, "bf16": torch.bfloat16, "bfloat16": torch.bfloat16,
-         "fp16": torch.float16, "float16": torch.float16}
+         "fp16": torch.float16, "float16": torch.float16, "int8": torch.int8}
 
 
 def _rows(cols):
@@ -36,9 +40,10 @@ def _rows(cols):
 
 
 def _padded_dim(d, dtype):
-    """The engine's score GEMM takes power-of-two D >= 32 (>= 64 for fp16
-    screening); other D are zero-padded, which changes no dot product."""
-    p = 64 if dtype == torch.float16 else 32
+    """The engine's score GEMM takes power-of-two D >= 32 (>= 64 for fp16,
+    >= 256 for int8 screening); other D are zero-padded, which changes no dot
+    product."""
+    p = 64 if dtype == torch.float16 else 256 if dtype == torch.int8 else 32
     while p < d:
         p <<= 1
     return p

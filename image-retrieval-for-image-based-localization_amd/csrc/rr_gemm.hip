@@ -619,11 +619,16 @@ static void launch_cfg3(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
 // Tiles are assigned XCD-contiguously (bijective remap): the pixel tiles of
 // one channel tile (e.g. the query tiles of one database tile in the kNN
 // score GEMM) share their A rows in one XCD's L2.  One tile per block.
+// T = int8_t: the kNN screening GEMM on int8-quantised rows (v_mfma_i32_16x16x64_i8,
+// twice the bf16 MFMA rate, half the bytes per row): a 128-B K-step is 128 elements
+// (two 64-deep MFMAs), the accumulators are exact int32 and the epilogue converts
+// them to float (K1, natural row order, float out only).
 template <typename T, typename TO, int KM, bool PERM>
 __global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int ntiles) {
-    static_assert(sizeof(T) == 2, "16-bit operands");
+    constexpr bool I8 = std::is_same<T, int8_t>::value;
+    static_assert(sizeof(T) == 2 || (I8 && KM == 1 && !PERM && sizeof(TO) == 4), "16-bit operands / int8 scores");
     constexpr bool K1 = KM == 1, tapu = KM == 2;
-    constexpr int VEC = 8, ESZ = 2, HT = 16384, SS_MAX = 2048;
+    constexpr int ESZ = sizeof(T), VEC = 16 / ESZ, KSE = 128 / ESZ, HT = 16384, SS_MAX = 2048;
     // [buf E/O][A0, A1, B0, B1] + folded BN scale / shift of up to 2048 channels
     __shared__ __attribute__((aligned(1024))) char smem[8 * HT + 2 * SS_MAX * 4];
 
@@ -667,7 +672,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int n
     if (li >= n_x) return;
     const int H = a.h, W = a.w_, Cin = a.cin;
     const unsigned tap_magic = tapu_magic(a.kh * a.kw);  // tapu_k0
-    const int nk = a.kp / 64;
+    const int nk = a.kp / KSE;
     const unsigned lds0 = (unsigned)(unsigned long long)smem;
     const int lrow = lane >> 3, lchunk = (lane & 7) ^ (lrow & 7);
 
@@ -716,7 +721,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int n
     auto kdesc = [&](int kt) {
         KD d;
         d.live = kt < nk;
-        d.k0 = tapu ? tapu_k0(kt, a.kh * a.kw, tap_magic, Cin >> 6, Cin, 64) : kt * 64;
+        d.k0 = tapu ? tapu_k0(kt, a.kh * a.kw, tap_magic, Cin >> 6, Cin, 64) : kt * KSE;
         d.dh = d.dw = d.add = 0;
         if constexpr (tapu) {
             const int tap = d.k0 >> a.lc, ci0 = d.k0 & (Cin - 1);
@@ -733,7 +738,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int n
         if (X < 2) {
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                const unsigned off = (d.live && a_off[X][i] != OOB) ? a_off[X][i] + (unsigned)(d.k0 * 2) : OOB;
+                const unsigned off = (d.live && a_off[X][i] != OOB) ? a_off[X][i] + (unsigned)(d.k0 * ESZ) : OOB;
                 dma16(rsA, off, dst + (wave + 8 * i) * 1024);
             }
         } else {
@@ -793,7 +798,11 @@ __global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int n
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
-                    if constexpr (std::is_same<T, f16_t>::value)
+                    if constexpr (I8)
+                        acc[qa][qb][i][j] = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_mfma_i32_16x16x64_i8(
+                            __builtin_bit_cast(i32x4_t, fa[i][hs]), __builtin_bit_cast(i32x4_t, fb[j][hs]),
+                            __builtin_bit_cast(i32x4_t, acc[qa][qb][i][j]), 0, 0, 0));
+                    else if constexpr (std::is_same<T, f16_t>::value)
                         acc[qa][qb][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
                             __builtin_bit_cast(f16x8_t, fa[i][hs]), __builtin_bit_cast(f16x8_t, fb[j][hs]),
                             acc[qa][qb][i][j], 0, 0, 0);
@@ -898,7 +907,9 @@ __global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int n
                             if (ok) tau = tau_lds ? lds_tau[p] : a.scr_tau[p];
                             float v[4];
 #pragma unroll
-                            for (int r = 0; r < 4; ++r) v[r] = acc[qa][qb][i][j][r] * 1.f + 0.f;  // (as the affine-free store path)
+                            for (int r = 0; r < 4; ++r)  // (as the affine-free store path)
+                                v[r] = I8 ? (float)__builtin_bit_cast(i32x4_t, acc[qa][qb][i][j])[r]
+                                          : acc[qa][qb][i][j][r] * 1.f + 0.f;
                             st.add(a, v, c, a.cout, p, ok, tau);
                         }
             st.flush(a);
@@ -980,7 +991,9 @@ __global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int n
                         if (p >= a.P) continue;
                         float v[4];
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) v[r] = acc[qa][qb][i][j][r] * sc[r] + sh[r];
+                        for (int r = 0; r < 4; ++r)
+                            v[r] = I8 ? (float)__builtin_bit_cast(i32x4_t, acc[qa][qb][i][j])[r]
+                                      : acc[qa][qb][i][j][r] * sc[r] + sh[r];
                         if constexpr (sizeof(TO) == 4) {
                             if (a.scr_k) {  // kNN screen: append survivors, store nothing
                                 screen_append(a, v, c, a.cout, p, a.scr_tau[p]);
@@ -1200,10 +1213,13 @@ __global__ void __launch_bounds__(512, 1) k_gemm8h(ConvArgs a, int ntiles) {
 // vmcnt: per stream position the block issues 2 query DMAs (asm, not counted
 // by the compiler) and then 4 DB loads (compiler-visible); position f's query
 // stage is complete once at most 6 (R - 1) + 4 younger operations remain.
+// T = int8_t: int8-quantised rows on v_mfma_i32_16x16x64_i8 (see k_gemm8): the same
+// 128-B K-steps carry 128 elements, accumulators are exact int32, scores float(acc).
 template <typename T, int R>
 __global__ void __launch_bounds__(512, 1) k_gemm8s(ConvArgs a, int ntiles) {
-    static_assert(sizeof(T) == 2 && 6 * (R - 1) + 4 <= 63, "16-bit operands, vmcnt range");
-    constexpr int ESZ = 2, HT = 16384, NB = R + 1;
+    constexpr bool I8 = std::is_same<T, int8_t>::value;
+    static_assert((sizeof(T) == 2 || I8) && 6 * (R - 1) + 4 <= 63, "16-bit / int8 operands, vmcnt range");
+    constexpr int ESZ = sizeof(T), VEC = 16 / ESZ, HT = 16384, NB = R + 1;
     // query stages + the queries' thresholds (<= 128) + 8 survivor lists (ScreenStage)
     __shared__ __attribute__((aligned(1024))) char smem[NB * HT + 4 * (128 + 8 * 3 * ScreenStage::CAP)];
 
@@ -1217,7 +1233,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm8s(ConvArgs a, int ntiles) {
     const int li = bx >> 3;
     if (li >= n_x) return;
     const int my = (n_x - li + nb_x - 1) / nb_x;  // tiles of this block: s_x + li + m * nb_x
-    const int nk = a.kp / 64;
+    const int nk = a.kp * ESZ / 128;
     const int F = my * nk;                        // (tile, K-step) stream of this block
     const unsigned lds0 = (unsigned)(unsigned long long)smem;
     const int lrow = lane >> 3, lchunk = (lane & 7) ^ (lrow & 7);
@@ -1228,7 +1244,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm8s(ConvArgs a, int ntiles) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int p = (wave + 8 * i) * 8 + lrow;
-        b_off[i] = p < a.P ? (unsigned)(((long long)p * a.cin + lchunk * 8) * ESZ) : OOB;
+        b_off[i] = p < a.P ? (unsigned)(((long long)p * a.cin + lchunk * VEC) * ESZ) : OOB;
     }
     uint32_t* const lds_tau = reinterpret_cast<uint32_t*>(smem + NB * HT);
     uint32_t* const lds_stage = lds_tau + 128;
@@ -1301,7 +1317,11 @@ __global__ void __launch_bounds__(512, 1) k_gemm8s(ConvArgs a, int ntiles) {
                 for (int hs = 0; hs < 2; ++hs)
 #pragma unroll
                     for (int g = 0; g < 2; ++g) {
-                        if constexpr (std::is_same<T, f16_t>::value)
+                        if constexpr (I8)
+                            acc[g][j] = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_mfma_i32_16x16x64_i8(
+                                __builtin_bit_cast(i32x4_t, ar[u][g][hs]), __builtin_bit_cast(i32x4_t, fb[hs]),
+                                __builtin_bit_cast(i32x4_t, acc[g][j]), 0, 0, 0));
+                        else if constexpr (std::is_same<T, f16_t>::value)
                             acc[g][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
                                 __builtin_bit_cast(f16x8_t, ar[u][g][hs]), __builtin_bit_cast(f16x8_t, fb[hs]),
                                 acc[g][j], 0, 0, 0);
@@ -1326,7 +1346,8 @@ __global__ void __launch_bounds__(512, 1) k_gemm8s(ConvArgs a, int ntiles) {
                             const bool ok = p < a.P;
                             float v[4];
 #pragma unroll
-                            for (int r = 0; r < 4; ++r) v[r] = acc[g][j][r];
+                            for (int r = 0; r < 4; ++r)
+                                v[r] = I8 ? (float)__builtin_bit_cast(i32x4_t, acc[g][j])[r] : acc[g][j][r];
                             st.add(a, v, c0 + 32 * wave + 16 * g + 4 * kq, a.cout, p, ok, ok ? lds_tau[p] : 0xffffffffu);
                         }
                     st.flush(a);
@@ -1342,7 +1363,8 @@ __global__ void __launch_bounds__(512, 1) k_gemm8s(ConvArgs a, int ntiles) {
                         if (p >= a.P) continue;
                         float v[4];
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) v[r] = acc[g][j][r];
+                        for (int r = 0; r < 4; ++r)
+                            v[r] = I8 ? (float)__builtin_bit_cast(i32x4_t, acc[g][j])[r] : acc[g][j][r];
                         acc[g][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
                         const long long o = (long long)p * a.ldy + c;
                         if (full) {
@@ -1725,6 +1747,29 @@ static bool try_gemm8a(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
         else hipLaunchKernelGGL((k_gemm8a<T, 2>), dim3(ntiles), dim3(512), 0, s, a, tiles_p, ntiles);
         return true;
     }
+}
+
+// kNN score GEMM on int8-quantised rows (float scores = exact int32 dot products):
+// k_gemm8s at <= 128 queries (streaming the database), persistent k_gemm8 above.
+// Needs 128-B K-steps (d % 128 == 0) and, for k_gemm8, an even K-step count.
+int gemm_scores_i8(const ConvArgs& a, hipStream_t s) {
+    if (a.kp != a.cin || a.kp % 128 || a.P < 1 || (long long)a.P * a.cin >= (1ll << 31) ||
+        256ll * a.kp >= (1ll << 31))
+        return fail(RR_EINVAL, "int8 score GEMM: d must be a multiple of 128 (rows and queries below 2 GiB)");
+    const long long cus = grid_cus();
+    if (a.P <= 128) {
+        const long long ntiles = ((long long)a.cout + 255) / 256;
+        const unsigned g = (unsigned)(cus < 8 || ntiles < cus ? ntiles : cus);
+        hipLaunchKernelGGL((k_gemm8s<int8_t, 4>), dim3(g), dim3(512), 0, s, a, (int)ntiles);
+        return RR_OK;
+    }
+    if ((a.kp / 128) & 1) return fail(RR_EINVAL, "int8 score GEMM above 128 queries: d must be a multiple of 256");
+    const int tiles_p = (a.P + 255) / 256;
+    const long long ntiles = (long long)tiles_p * ((a.cout + 255) / 256);
+    if (ntiles >= (1ll << 31)) return fail(RR_EINVAL, "int8 score GEMM: too many tiles");
+    const dim3 g((unsigned)(cus < 8 || ntiles < cus ? ntiles : cus));
+    hipLaunchKernelGGL((k_gemm8<int8_t, float, 1, false>), g, dim3(512), 0, s, a, tiles_p, (int)ntiles);
+    return RR_OK;
 }
 
 int g_force_cfg = 0;  // rr_set_tuning(RR_TUNE_GEMM_CONFIG, ...)

@@ -252,6 +252,8 @@ struct ScreenStage {
 };
 // scores[p][c] (f32, row stride ldy) = x[p][:] . w[c][:], 1x1 GEMM, dtype in.
 void gemm_scores(const ConvArgs& a, int dtype, hipStream_t s);
+// the same on int8-quantised rows (rr_gemm.hip): float(exact int32 dot product)
+int gemm_scores_i8(const ConvArgs& a, hipStream_t s);
 
 // RR_CONV_PERM32 row order: packed row g*32 + i*16 + 4q + r holds channel g*32 + 8q + 4i + r.
 __host__ __device__ __forceinline__ int perm32_channel(int packed_row) {

@@ -22,6 +22,7 @@
 #include "rr_internal.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace rr {
 
@@ -507,7 +508,20 @@ template <typename T>
 __device__ __forceinline__ void fixup_scores(const T* __restrict__ dr, bool row_ok, const T* __restrict__ qr, bool col0,
                                              int d, f32x4_knn_t& acc) {
     const int kq = (threadIdx.x & 63) >> 4;
-    if constexpr (sizeof(T) == 2) {
+    if constexpr (std::is_same<T, int8_t>::value) {  // int8 rows: exact int32 dot products (any order)
+        typedef __attribute__((ext_vector_type(4))) int i32x4_knn_t;
+        for (int k0 = 0; k0 < d; k0 += 128) {
+#pragma unroll
+            for (int hs = 0; hs < 2; ++hs) {
+                const int off = k0 + (kq + 4 * hs) * 16;
+                const uint4 av = row_ok ? *reinterpret_cast<const uint4*>(dr + off) : make_uint4(0, 0, 0, 0);
+                const uint4 bv = col0 ? *reinterpret_cast<const uint4*>(qr + off) : make_uint4(0, 0, 0, 0);
+                acc = __builtin_bit_cast(f32x4_knn_t, __builtin_amdgcn_mfma_i32_16x16x64_i8(
+                    __builtin_bit_cast(i32x4_knn_t, av), __builtin_bit_cast(i32x4_knn_t, bv),
+                    __builtin_bit_cast(i32x4_knn_t, acc), 0, 0, 0));
+            }
+        }
+    } else if constexpr (sizeof(T) == 2) {
         for (int k0 = 0; k0 < d; k0 += 64) {
 #pragma unroll
             for (int hs = 0; hs < 2; ++hs) {
@@ -555,7 +569,9 @@ __global__ void __launch_bounds__(SEL_THREADS) k_slot_fixup(const T* __restrict_
             if (r16 == 0) {  // D[row 4 kq + e][column 0]
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
-                    if (g + 4 * kq + e < len) keys[g + 4 * kq + e] = score_key(acc[e] * 1.f + 0.f);  // as the GEMM epilogue (-0 -> +0)
+                    if (g + 4 * kq + e < len)  // as the GEMM epilogue (-0 -> +0; int8: float of the exact int32)
+                        keys[g + 4 * kq + e] = score_key(std::is_same<T, int8_t>::value
+                                                             ? (float)__float_as_int(acc[e]) : acc[e] * 1.f + 0.f);
             }
         }
         __syncthreads();
@@ -691,7 +707,9 @@ struct KnnPlan {
 };
 
 static int default_cand(int k, int dtype) {
-    int extra = dtype == RR_BF16 ? 128 : dtype == RR_F16 ? 64 : 32;  // screening error: bf16 ~1e-4, fp16 ~1e-5
+    // screening error: bf16 ~5e-5, fp16 ~1e-5, int8 ~4e-4 (std on unit 2048-d rows; at 1M random rows
+    // the true top 100 lie within the first 118 int8-ordered rows, 32 queries measured)
+    int extra = dtype == RR_BF16 || dtype == RR_I8 ? 128 : dtype == RR_F16 ? 64 : 32;
     return ((k + extra + 63) / 64) * 64;
 }
 
@@ -744,8 +762,11 @@ int rr_knn_topk_checked(const void* db, const float* db_f32, long long n_db, con
                         void* stream) {
     if (n_db <= 0 || nq <= 0 || k <= 0) return fail(RR_EINVAL, "rr_knn_topk: empty problem");
     if (n_db > 0x7fffffffll) return fail(RR_EINVAL, "rr_knn_topk: shard rows must fit int32 (shard the database)");
-    if (dtype != RR_BF16 && dtype != RR_F32 && dtype != RR_F16) return fail(RR_EINVAL, "rr_knn_topk: dtype");
+    if (dtype != RR_BF16 && dtype != RR_F32 && dtype != RR_F16 && dtype != RR_I8)
+        return fail(RR_EINVAL, "rr_knn_topk: dtype");
     if (dtype == RR_F16 && d < 64) return fail(RR_EINVAL, "rr_knn_topk: fp16 screening needs d >= 64");
+    if (dtype == RR_I8 && (d < 128 || (nq > 128 && d < 256)))
+        return fail(RR_EINVAL, "rr_knn_topk: int8 screening needs d >= 128 (d >= 256 above 128 queries)");
     if (d <= 0 || d % 32 || (d & (d - 1))) return fail(RR_EINVAL, "rr_knn_topk: d must be a power of two >= 32");
     KnnPlan p = plan(n_db, nq, k, cand, dtype);
     if (p.KC < k) return fail(RR_EINVAL, "rr_knn_topk: cand must be >= k");
@@ -771,12 +792,14 @@ int rr_knn_topk_checked(const void* db, const float* db_f32, long long n_db, con
         (void)hipFuncSetAttribute((const void*)k_slot_fixup<bf16_t>, hipFuncAttributeMaxDynamicSharedMemorySize, CHUNK_L * 4);
         (void)hipFuncSetAttribute((const void*)k_slot_fixup<f16_t>, hipFuncAttributeMaxDynamicSharedMemorySize, CHUNK_L * 4);
         (void)hipFuncSetAttribute((const void*)k_slot_fixup<float>, hipFuncAttributeMaxDynamicSharedMemorySize, CHUNK_L * 4);
+        (void)hipFuncSetAttribute((const void*)k_slot_fixup<int8_t>, hipFuncAttributeMaxDynamicSharedMemorySize, CHUNK_L * 4);
         (void)hipFuncSetAttribute((const void*)k_final_sort, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 4096);
         (void)hipFuncSetAttribute((const void*)k_merge, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 4096);
         attr_done = true;
     }
 
-    const size_t esz = dtype == RR_F32 ? 4 : 2;
+    const size_t esz = dtype == RR_F32 ? 4 : dtype == RR_I8 ? 1 : 2;
+    auto scores = [&](const ConvArgs& a) { return dtype == RR_I8 ? gemm_scores_i8(a, s) : (gemm_scores(a, dtype, s), RR_OK); };
     // Screening (default): the first PREFIX_CHUNKS chunks go through the score
     // slab + chunk select, which sets each query's running threshold tau; the
     // rest of the database is ONE score GEMM whose epilogue appends only the
@@ -812,7 +835,7 @@ int rr_knn_topk_checked(const void* db, const float* db_f32, long long n_db, con
     };
     for (long long r0 = 0; r0 < slab_rows; r0 += (long long)p.G * p.L) {
         const int rows = (int)((slab_rows - r0) < (long long)p.G * p.L ? (slab_rows - r0) : (long long)p.G * p.L);
-        gemm_scores(score_args(r0, rows), dtype, s);
+        if (int rc = scores(score_args(r0, rows))) return rc;
         const int chunks = (rows + p.L - 1) / p.L;
         hipLaunchKernelGGL(k_chunk_select, dim3(nq, chunks), dim3(SEL_THREADS), (size_t)p.L * 4, s, slab, p.S, p.L,
                            rows, (int)r0, (int)(r0 / p.L), p.nchunks, p.KC, cand_k, cand_i, tau);
@@ -822,7 +845,7 @@ int rr_knn_topk_checked(const void* db, const float* db_f32, long long n_db, con
         ConvArgs a = score_args(slab_rows, (int)(n_db - slab_rows));
         a.scr_tau = tau; a.scr_cnt = cnt; a.scr_k = cand_k; a.scr_i = cand_i;
         a.scr_L = p.L; a.scr_nchunks = p.nchunks; a.scr_KC = p.KC; a.scr_row0 = (int)slab_rows;
-        gemm_scores(a, dtype, s);
+        if (int rc = scores(a)) return rc;
         const dim3 g(nq), b(SEL_THREADS);
         const size_t lds = (size_t)p.L * 4;
         if (dtype == RR_BF16)
@@ -830,6 +853,9 @@ int rr_knn_topk_checked(const void* db, const float* db_f32, long long n_db, con
                                p.nchunks, g0, p.KC, cnt, cand_k, cand_i, tau);
         else if (dtype == RR_F16)
             hipLaunchKernelGGL(k_slot_fixup<f16_t>, g, b, lds, s, (const f16_t*)db, n_db, (const f16_t*)q, d, p.L,
+                               p.nchunks, g0, p.KC, cnt, cand_k, cand_i, tau);
+        else if (dtype == RR_I8)
+            hipLaunchKernelGGL(k_slot_fixup<int8_t>, g, b, lds, s, (const int8_t*)db, n_db, (const int8_t*)q, d, p.L,
                                p.nchunks, g0, p.KC, cnt, cand_k, cand_i, tau);
         else
             hipLaunchKernelGGL(k_slot_fixup<float>, g, b, lds, s, (const float*)db, n_db, (const float*)q, d, p.L,
@@ -847,8 +873,11 @@ int rr_knn_topk_checked(const void* db, const float* db_f32, long long n_db, con
     // screening error bound per unit ||q|| ||x||: input rounding of both
     // operands (bf16 2^-9, fp16 2^-11 relative each; products exact in f32)
     // plus f32 accumulation over d terms (d 2^-24)
+    // int8 scores are integer dot products (no common scale with the exact scores):
+    // no certificate, every query with more than k rows is flagged
     const double in_eps = dtype == RR_BF16 ? 0x1p-8 + 0x1p-17 : dtype == RR_F16 ? 0x1p-10 + 0x1p-21 : 0.0;
-    const double delta_scale = (in_eps + d * 0x1p-24) * 1.001 * (db_norm_max > 0.f ? db_norm_max : 1.0);
+    const double delta_scale = dtype == RR_I8 ? (double)INFINITY
+                                              : (in_eps + d * 0x1p-24) * 1.001 * (db_norm_max > 0.f ? db_norm_max : 1.0);
     hipLaunchKernelGGL(k_final_sort, dim3(nq), dim3(SEL_THREADS), fin_lds, s, fin_s, fin_i, p.npow2, k, idx_offset,
                        out_scores, out_idx, sel_thr, q_f32, d, delta_scale, out_uncertain);
     return check_launch("rr_knn_topk");

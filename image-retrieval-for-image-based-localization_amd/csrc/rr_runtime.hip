@@ -305,6 +305,47 @@ __global__ void k_cast_f32_bf16(const float* __restrict__ x, bf16_t* __restrict_
     }
 }
 
+// int8 screening copy (rr_quantize_i8): amax = max |x| (non-negative floats order
+// like their bit patterns: one unsigned atomicMax per block), then
+// y = clamp(rint(x * 127 / amax), -127, 127) with the scale read on the device.
+__global__ void k_amax_reset(unsigned* amax) { *amax = 0u; }
+
+__global__ void __launch_bounds__(256) k_absmax(const float* __restrict__ x, long long n, unsigned* __restrict__ amax) {
+    const long long step = (long long)gridDim.x * blockDim.x * 4;
+    float m = 0.f;
+    for (long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += step) {
+        if (i + 3 < n) {
+            const float4 v = *reinterpret_cast<const float4*>(x + i);
+            m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+        } else {
+            for (long long j = i; j < n; ++j) m = fmaxf(m, fabsf(x[j]));
+        }
+    }
+    m = wave_max(m);
+    __shared__ float red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(amax, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+}
+
+__global__ void __launch_bounds__(256) k_cast_f32_i8(const float* __restrict__ x, long long n,
+                                                     const unsigned* __restrict__ amax, int8_t* __restrict__ y) {
+    const float am = __uint_as_float(*amax);
+    const float sc = am > 0.f ? 127.f / am : 1.f;
+    auto q = [&](float v) { return (int)fminf(fmaxf(rintf(v * sc), -127.f), 127.f); };
+    const long long step = (long long)gridDim.x * blockDim.x * 4;
+    for (long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += step) {
+        if (i + 3 < n) {
+            const float4 v = *reinterpret_cast<const float4*>(x + i);
+            const unsigned w = (unsigned)(q(v.x) & 255) | ((unsigned)(q(v.y) & 255) << 8) |
+                               ((unsigned)(q(v.z) & 255) << 16) | ((unsigned)(q(v.w) & 255) << 24);
+            *reinterpret_cast<unsigned*>(y + i) = w;
+        } else {
+            for (long long j = i; j < n; ++j) y[j] = (int8_t)q(x[j]);
+        }
+    }
+}
+
 static inline unsigned cast_blocks(long long n) {
     const long long b = (n + 1023) / 1024;       // 256 threads x 4 elements
     return (unsigned)(b < (1ll << 20) ? (b > 0 ? b : 1) : (1ll << 20));
@@ -473,6 +514,19 @@ int rr_cast_f32_f16(const float* x, void* y, long long n, void* stream) {
     hipLaunchKernelGGL(k_cast_f32_f16, dim3(cast_blocks(n)), dim3(256), 0, as_stream(stream), x,
                        (f16_t*)y, n);
     return check_launch("rr_cast_f32_f16");
+}
+
+int rr_quantize_i8(const float* x, long long n, void* y, float* amax_dev, void* stream) {
+    if (n <= 0) return RR_OK;
+    if (!x || !y || !amax_dev) return fail(RR_EINVAL, "rr_quantize_i8: null pointer");
+    if (n % 4 || ((uintptr_t)x & 15) || ((uintptr_t)y & 3)) return fail(RR_EINVAL, "rr_quantize_i8: n % 4, alignment");
+    hipStream_t s = as_stream(stream);
+    const unsigned g = cast_blocks(n) < 4096u ? cast_blocks(n) : 4096u;
+    hipLaunchKernelGGL(k_amax_reset, dim3(1), dim3(1), 0, s, (unsigned*)amax_dev);
+    hipLaunchKernelGGL(k_absmax, dim3(g), dim3(256), 0, s, x, n, (unsigned*)amax_dev);
+    hipLaunchKernelGGL(k_cast_f32_i8, dim3(cast_blocks(n)), dim3(256), 0, s, x, n, (const unsigned*)amax_dev,
+                       (int8_t*)y);
+    return check_launch("rr_quantize_i8");
 }
 
 int rr_cast_f32_bf16(const float* x, void* y, long long n, void* stream) {

@@ -44,6 +44,11 @@ struct StemArgs {
 };
 
 constexpr int NT = 512;  // threads per block (8 waves)
+// packed stem weights: [64 rows (PERM32)][448] 16-bit = 56 x 16-B chunks per row:
+// k < 256: kernel-row layout (k = kh*32 + kw*4 + ci) of v1-v3; k in [256, 448):
+// the space-to-depth layout of v4 (k' = kr*48 + kc*12 + a*6 + b*3 + ci, kh = 2kr + a,
+// kw = 2kc + b)
+constexpr int WROW = 56, W4OFF = 32;
 
 typedef __attribute__((ext_vector_type(2))) short short2v;
 
@@ -84,7 +89,7 @@ __global__ void __launch_bounds__(NT) k_stem_pool(StemArgs a, TAB rt, int tiles_
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int m = 0; m < 7; ++m) areg[i][m] = a.w[(i * 16 + r16) * 32 + m * 4 + q];
+        for (int m = 0; m < 7; ++m) areg[i][m] = a.w[(i * 16 + r16) * WROW + m * 4 + q];
 
     auto tile_origin = [&](int t, int& img, int& ph0, int& pw0) {
         img = t / tiles_hw;
@@ -291,7 +296,7 @@ __global__ void __launch_bounds__(NT) k_stem_pool2(StemArgs a, int tiles_w, int 
         const unsigned flip = a.scale[perm32_channel(i * 16 + r16)] < 0.f ? 0x80008000u : 0u;
 #pragma unroll
         for (int m = 0; m < 7; ++m) {
-            uint4 w = a.w[(i * 16 + r16) * 32 + m * 4 + q];
+            uint4 w = a.w[(i * 16 + r16) * WROW + m * 4 + q];
             w.x ^= flip; w.y ^= flip; w.z ^= flip; w.w ^= flip;
             areg[i][m] = w;
         }
@@ -543,7 +548,7 @@ __global__ void __launch_bounds__(NT) k_stem_pool3(StemArgs a, TAB rt, int tiles
         const unsigned flip = s < 0.f ? 0x80008000u : 0u;
 #pragma unroll
         for (int m = 0; m < 7; ++m) {
-            uint4 w = a.w[R * 32 + m * 4 + q];
+            uint4 w = a.w[R * WROW + m * 4 + q];
             w.x ^= flip; w.y ^= flip; w.z ^= flip; w.w ^= flip;
             breg[f][m] = w;
         }
@@ -739,14 +744,277 @@ __global__ void __launch_bounds__(NT) k_stem_pool3(StemArgs a, TAB rt, int tiles
 }
 
 
-// out[R][k], R packed row (PERM32), k = kh*32 + kw*4 + ci (kh < 7, kw < 7, ci < 3 real; rest 0)
+// ---------------------------------------------------------------------------
+// Stem v4: v3's tile, wave layout, lane-local pooling and epilogue, with the
+// conv's K in space-to-depth form.  The stride-2 7x7 conv on 3 channels is a
+// stride-1 4x4 conv on 12-channel "s2d pixels" (2x2 input pixels x 3 channels,
+// the 8x8-padded kernel: kh = 7 / kw = 7 carry zero weights): K = 4 x 4 x 12 =
+// 192 = 6 MFMA K-steps of 32 instead of v3's 7 (7 kernel rows x 8 pixels x 4
+// channels, 66 % of it useful; here 77 %).  The patch sits in LDS as s2d pixels
+// of 24 B ([s2d row][s2d col][a][b][ci], a / b = row / column in the pair): the 4
+// s2d pixels of one kernel row are 48 contiguous values, so a lane's 8 values of
+// a K-step (k0 = 32 m + 8 q; a kernel row holds 48, a multiple of 8) are 16
+// contiguous bytes at an 8-B aligned address: two ds_read_b64.  The tile's s2d
+// rows and columns start one before its first stem row / column (stem pixel c
+// uses s2d columns c - 1 .. c + 2); the patch (20 x 117 s2d pixels, 56 KiB) covers
+// the same input rectangle as v3's (4 ph0 - 5 .., 4 pw0 - 5 ..), plus the one input
+// row under the zero kh = 7 weights.  Same value per tap as v3 (normalised,
+// rounded to 16 bits, zero padding after normalisation); only the f32 summation
+// order of the 147 products differs.
+template <typename HT, bool U8, int NPART, typename TAB = NoTab>
+__global__ void __launch_bounds__(NT) k_stem_pool4(StemArgs a, TAB rt, int tiles_w, int tiles_hw, int ntiles) {
+    constexpr bool RG = std::is_same<TAB, RaggedTab>::value;
+    constexpr int PH = 8, PW = 56, SRN = 2 * PH + 1, CB = 14;
+    constexpr int SCN = CB * 7 + 16;                 // 114 stem columns
+    constexpr int PR = SRN + 3, PC = SCN + 3;        // 20 x 117 s2d pixels
+    constexpr int SP = 24;                           // bytes per s2d pixel (12 x 16-bit)
+    constexpr int NPIX = PR * PC, PPT = (NPIX + NT - 1) / NT;
+    constexpr int PATCH = NPIX * SP;
+    static_assert(PW == 7 * (NT / 64), "one 7-pooled-column block per wave");
+    __shared__ __attribute__((aligned(16))) char sP[2][PATCH];
+    __shared__ float sL[U8 ? 3 * 256 : 1];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r16 = lane & 15, q = lane >> 4;
+    const int H = a.h, W = a.w_;
+    const long long plane = (long long)H * W;
+
+    if constexpr (U8) {
+        for (int i = tid; i < 3 * 256; i += NT) {
+            const int ch = i >> 8;
+            const float x = (float)(i & 255) / 255.f;  // IEEE division = to_tensor
+            sL[i] = a.do_norm ? (x - a.mean[ch]) * a.rstd[ch] : x;
+        }
+    }
+    // B fragments (channel 4 * r16 + f of fragment f, s2d K-step m), negative-scale
+    // channels negated (pool before the epilogue, see v2)
+    uint4 breg[4][6];
+    float sc[4], sh[4];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+        const int c = 4 * r16 + f;
+        const int R = (c & ~31) | (((c >> 2) & 1) << 4) | (((c >> 3) & 3) << 2) | (c & 3);  // perm32_channel^-1
+        const float s = a.scale[c];
+        sc[f] = fabsf(s);
+        sh[f] = a.shift[c];
+        const unsigned flip = s < 0.f ? 0x80008000u : 0u;
+#pragma unroll
+        for (int m = 0; m < 6; ++m) {
+            uint4 w = a.w[R * WROW + W4OFF + m * 4 + q];
+            w.x ^= flip; w.y ^= flip; w.z ^= flip; w.w ^= flip;
+            breg[f][m] = w;
+        }
+    }
+    // this lane's byte offset of K-step m inside the 4 x 4 s2d window of its pixel
+    int koff[6];
+#pragma unroll
+    for (int m = 0; m < 6; ++m) {
+        const int k0 = 32 * m + 8 * q;
+        koff[m] = (k0 / 48) * (PC * SP) + (k0 % 48) * 2;
+    }
+
+    auto tile_origin = [&](int t, int& img, int& ph0, int& pw0) {
+        img = t / tiles_hw;
+        const int rem = t - img * tiles_hw;
+        const int th = rem / tiles_w;
+        ph0 = th * PH;
+        pw0 = (rem - th * tiles_w) * PW;
+    };
+
+    // patch fill in NPART parts: work item = one s2d pixel (2 input rows x 2 columns x 3 channels)
+    constexpr int PH1 = (PPT + NPART - 1) / NPART;
+    typedef typename std::conditional<U8, int, float>::type PT;
+    PT pf[PH1][12];
+    auto fill_load = [&](int t, int part) {
+        int img, ph0, pw0;
+        tile_origin(t, img, ph0, pw0);
+        const int ir0 = 4 * ph0 - 5, ic0 = 4 * pw0 - 5;
+        constexpr int ESZ = U8 ? 1 : 4;
+        constexpr unsigned OOBO = 0x80000000u;
+        const char* ib;
+        int hi = H, wi = W;
+        if constexpr (RG) {
+            ib = (const char*)rt.p[img];
+            hi = rt.h[img];
+            wi = rt.w[img];
+        } else {
+            ib = (const char*)a.x + (long long)img * 3 * plane * ESZ;
+        }
+        const int iplane = hi * wi;
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc((void*)ib, (short)0, (int)(3 * iplane * ESZ), 0x00020000);
+#pragma unroll
+        for (int uu = 0; uu < PH1; ++uu) {
+            const int u = part * PH1 + uu;
+            if (u >= PPT) break;
+            int k = tid + NT * u;
+            asm volatile("" : "+v"(k));  // offsets computed here, not hoisted into live VGPRs
+            const int kk = k < NPIX ? k : NPIX - 1;
+            const int r = kk / PC, c = kk - r * PC;
+            const int ih = ir0 + 2 * r, iw = ic0 + 2 * c;
+            unsigned off[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {  // e = a * 2 + b
+                const int y = ih + (e >> 1), x = iw + (e & 1);
+                off[e] = ((unsigned)y < (unsigned)hi && (unsigned)x < (unsigned)wi) ? (unsigned)((y * wi + x) * ESZ)
+                                                                                     : OOBO;
+            }
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) {
+                const unsigned po = (unsigned)(ch * iplane * ESZ);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    if constexpr (U8)
+                        pf[uu][e * 3 + ch] = ch * 256 + (int)__builtin_amdgcn_raw_buffer_load_b8(rs, (int)(off[e] + po), 0, 0);
+                    else
+                        pf[uu][e * 3 + ch] =
+                            __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(off[e] + po), 0, 0));
+                }
+            }
+        }
+    };
+    auto fill_store = [&](int t, int buf, int part) {
+        int img, ph0, pw0;
+        tile_origin(t, img, ph0, pw0);
+        const int ir0 = 4 * ph0 - 5, ic0 = 4 * pw0 - 5;
+#pragma unroll
+        for (int uu = 0; uu < PH1; ++uu) {
+            const int u = part * PH1 + uu;
+            if (u >= PPT) break;
+            int k = tid + NT * u;
+            asm volatile("" : "+v"(k));
+            if (k >= NPIX) continue;
+            const int r = k / PC, c = k - r * PC;
+            float v[12];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const bool ok = (unsigned)(ir0 + 2 * r + (e >> 1)) < (unsigned)H &&
+                                (unsigned)(ic0 + 2 * c + (e & 1)) < (unsigned)W;
+#pragma unroll
+                for (int ch = 0; ch < 3; ++ch) {  // zero padding is applied AFTER normalisation
+                    float x;
+                    if constexpr (U8) x = sL[pf[uu][e * 3 + ch]];
+                    else x = a.do_norm ? (pf[uu][e * 3 + ch] - a.mean[ch]) * a.rstd[ch] : pf[uu][e * 3 + ch];
+                    v[e * 3 + ch] = ok ? x : 0.f;
+                }
+            }
+            char* dst = sP[buf] + k * SP;
+            *reinterpret_cast<uint2*>(dst) = make_uint2(H16<HT>::pack2(v[0], v[1]), H16<HT>::pack2(v[2], v[3]));
+            *reinterpret_cast<uint2*>(dst + 8) = make_uint2(H16<HT>::pack2(v[4], v[5]), H16<HT>::pack2(v[6], v[7]));
+            *reinterpret_cast<uint2*>(dst + 16) = make_uint2(H16<HT>::pack2(v[8], v[9]), H16<HT>::pack2(v[10], v[11]));
+        }
+    };
+
+    const float slope = a.leaky ? a.slope : 1.f;  // identity == leaky with slope 1
+    const float NINF = -__builtin_inff();
+    int t = blockIdx.x;
+    if (t >= ntiles) return;
+    if constexpr (U8) __syncthreads();  // byte table
+#pragma unroll
+    for (int part = 0; part < NPART; ++part) {
+        fill_load(t, part);
+        fill_store(t, 0, part);
+    }
+    __syncthreads();
+    const int nb_addr = ((lane + 16) & 63) * 4;
+    int cur = 0;
+    for (; t < ntiles; t += gridDim.x, cur ^= 1) {
+        const int tn = t + gridDim.x;
+        if (tn < ntiles) fill_load(tn, 0);
+        int img, ph0, pw0;
+        tile_origin(t, img, ph0, pw0);
+        const char* pb = sP[cur] + (CB * wave + r16) * SP;
+        const bool active = pw0 + 7 * wave < a.wp;
+        const bool left = pw0 == 0 && wave == 0;
+        const int pc0 = 7 * wave + 2 * q;
+        const bool st0 = pw0 + pc0 < a.wp, st1 = q < 3 && pw0 + pc0 + 1 < a.wp;
+        auto stem_row = [&](int r, h16_f32x4_t (&acc)[4]) {
+#pragma unroll
+            for (int f = 0; f < 4; ++f) acc[f] = (h16_f32x4_t){0.f, 0.f, 0.f, 0.f};
+            const char* rb = pb + r * (PC * SP);
+#pragma unroll
+            for (int m = 0; m < 6; ++m) {
+                const uint2 lo = *reinterpret_cast<const uint2*>(rb + koff[m]);
+                const uint2 hi = *reinterpret_cast<const uint2*>(rb + koff[m] + 8);
+                const uint4 px = make_uint4(lo.x, lo.y, hi.x, hi.y);
+#pragma unroll
+                for (int f = 0; f < 4; ++f) acc[f] = H16<HT>::mfma(px, breg[f][m], acc[f]);
+            }
+        };
+        h16_f32x4_t A[4];
+        if (active) {
+            stem_row(0, A);
+            if (ph0 == 0) {  // stem row -1: max-pool padding
+#pragma unroll
+                for (int f = 0; f < 4; ++f) A[f] = (h16_f32x4_t){NINF, NINF, NINF, NINF};
+            }
+        }
+        for (int pr = 0; pr < PH; ++pr) {
+#pragma unroll
+            for (int part = 1; part < NPART; ++part)
+                if (pr == part * PH / NPART && tn < ntiles) {  // part - 1 of the next patch -> LDS, part in flight
+                    fill_store(tn, cur ^ 1, part - 1);
+                    fill_load(tn, part);
+                }
+            if (active) {
+                h16_f32x4_t B[4];
+                stem_row(2 * pr + 1, B);
+#pragma unroll
+                for (int f = 0; f < 4; ++f)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) A[f][e] = fmaxf(A[f][e], B[f][e]);  // rows 2pr, 2pr+1
+                h16_f32x4_t C[4];
+                stem_row(2 * pr + 2, C);
+                float p0[4], p1[4];
+#pragma unroll
+                for (int f = 0; f < 4; ++f) {
+                    float m3[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) m3[e] = fmaxf(A[f][e], C[f][e]);
+                    if (left && q == 0) m3[0] = NINF;  // stem column -1: max-pool padding
+                    const float nb = __int_as_float(__builtin_amdgcn_ds_bpermute(nb_addr, __float_as_int(m3[0])));
+                    p0[f] = fmaxf(fmaxf(m3[0], m3[1]), m3[2]);
+                    p1[f] = fmaxf(fmaxf(m3[2], m3[3]), nb);
+                    A[f] = C[f];
+                }
+                if (ph0 + pr < a.hp) {
+                    bf16_t* dst = a.y + (((long long)img * a.hp + ph0 + pr) * a.wp + pw0 + pc0) * 64 + 4 * r16;
+                    auto epi = [&](const float (&p)[4]) {
+                        float v[4];
+#pragma unroll
+                        for (int f = 0; f < 4; ++f) {
+                            v[f] = p[f] * sc[f] + sh[f];
+                            v[f] = fmaxf(v[f], v[f] * slope);
+                        }
+                        return make_uint2(H16<HT>::pack2(v[0], v[1]), H16<HT>::pack2(v[2], v[3]));
+                    };
+                    if (st0) *reinterpret_cast<uint2*>(dst) = epi(p0);
+                    if (st1) *reinterpret_cast<uint2*>(dst + 64) = epi(p1);
+                }
+            }
+        }
+        if (tn < ntiles) fill_store(tn, cur ^ 1, NPART - 1);
+        __syncthreads();
+    }
+}
+
+
+// out[R][k], R packed row (PERM32), k < 256: k = kh*32 + kw*4 + ci (kh < 7, kw < 7,
+// ci < 3 real; rest 0); k in [256, 448): the s2d order of v4 (see WROW)
 template <typename HT>
 __global__ void k_stem_pack(const float* __restrict__ w, HT* __restrict__ out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= 64 * 256) return;
-    const int R = i >> 8, k = i & 255;
+    if (i >= 64 * 448) return;
+    const int R = i / 448, k = i - R * 448;
     const int co = perm32_channel(R);
-    const int kh = k >> 5, kw = (k >> 2) & 7, ci = k & 3;
+    int kh, kw, ci;
+    if (k < 256) {
+        kh = k >> 5; kw = (k >> 2) & 7; ci = k & 3;
+    } else {
+        const int kk = k - 256, kr = kk / 48, kc = (kk % 48) / 12, j = kk % 12;
+        kh = 2 * kr + j / 6; kw = 2 * kc + (j % 6) / 3; ci = j % 3;
+    }
     float v = 0.f;
     if (kh < 7 && kw < 7 && ci < 3) v = w[((co * 3 + ci) * 7 + kh) * 7 + kw];
     out[i] = DT<HT>::from_f(v);
@@ -766,15 +1034,15 @@ extern "C" int rr_stem_pack_weights(const float* w, int c_out, int c_in, int kh,
     if (c_out != 64 || c_in != 3 || kh != 7 || kw != 7)
         return fail(RR_EINVAL, "rr_stem_pack_weights: the fused stem is the 3->64 7x7 conv1");
     if (dtype == RR_F16)
-        hipLaunchKernelGGL(k_stem_pack<f16_t>, dim3(64), dim3(256), 0, as_stream(stream), w, (f16_t*)out);
+        hipLaunchKernelGGL(k_stem_pack<f16_t>, dim3(112), dim3(256), 0, as_stream(stream), w, (f16_t*)out);
     else
-        hipLaunchKernelGGL(k_stem_pack<bf16_t>, dim3(64), dim3(256), 0, as_stream(stream), w, (bf16_t*)out);
+        hipLaunchKernelGGL(k_stem_pack<bf16_t>, dim3(112), dim3(256), 0, as_stream(stream), w, (bf16_t*)out);
     return check_launch("rr_stem_pack_weights");
 }
 
 namespace rr {
-int g_stem_mode = 2;  // rr_set_tuning(RR_TUNE_STEM): 2 swapped-operand lane-local pooling (v3),
-                      // 1 pool-before-epilogue kernel (v2), 0 k_stem_pool
+int g_stem_mode = 2;  // rr_set_tuning(RR_TUNE_STEM): 5 space-to-depth K (v4), 2 swapped-operand lane-local
+                      // pooling (v3; 3 / 4: 2 / 5 fill parts), 1 pool-before-epilogue kernel (v2), 0 k_stem_pool
 }
 
 // One launch over a same-size batch (TAB = NoTab, a.x = the [n][3][h][w] buffer)
@@ -792,7 +1060,10 @@ static void stem_launch(const StemArgs& a, const TAB& rt, int dtype, hipStream_t
             auto launch = [&](auto kern) {
                 hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), 0, st, a, rt, tiles_w, tiles_w * tiles_h, ntiles);
             };
-            if (dtype == RR_F16) {
+            if (g_stem_mode == 5) {
+                if (dtype == RR_F16) launch(k_stem_pool4<f16_t, U8, 3, TAB>);
+                else launch(k_stem_pool4<bf16_t, U8, 3, TAB>);
+            } else if (dtype == RR_F16) {
                 if (g_stem_mode == 3) launch(k_stem_pool3<f16_t, U8, 2, TAB>);
                 else if (g_stem_mode == 4) launch(k_stem_pool3<f16_t, U8, 5, TAB>);
                 else launch(k_stem_pool3<f16_t, U8, 3, TAB>);

@@ -27,7 +27,8 @@
 extern "C" {
 #endif
 
-enum rr_dtype { RR_F32 = 0, RR_BF16 = 1, RR_F16 = 2 };  /* 16-bit types: every conv kernel; RR_F16 also kNN screening */
+/* 16-bit types: every conv kernel; RR_F16 also kNN screening; RR_I8: kNN screening only (rr_quantize_i8) */
+enum rr_dtype { RR_F32 = 0, RR_BF16 = 1, RR_F16 = 2, RR_I8 = 3 };
 enum rr_act { RR_ACT_IDENTITY = 0, RR_ACT_LEAKY = 1 };
 enum rr_pool_mode { RR_POOL_GEM = 0, RR_POOL_MAC = 1, RR_POOL_SPOC = 2 };
 enum rr_conv_flags { RR_CONV_AFFINE = 1, RR_CONV_RESIDUAL = 2, RR_CONV_PERM32 = 4 };
@@ -118,7 +119,8 @@ int rr_maxpool2d(const void* x, int n, int h, int w, int c, int k, int stride, i
  * Sequential(conv1, bn1, pool1) of cirtorch/backbones/resnet.py:59-66 applied
  * to the output of utils/image.py:125 `normalize`.
  *   x     : [n][3][h][w] float32 (raw pixels when do_normalize, mean/std HOST arrays of 3)
- *   wpk   : rr_stem_pack_weights output, [64][256] (dtype)
+ *   wpk   : rr_stem_pack_weights output, [64][448] (dtype): the kernel-row layout (k < 256) and the
+ *           space-to-depth layout (k >= 256) of the two stem kernel families
  *   scale, shift : [64] float32 (folded BN), act RR_ACT_*, slope for leaky
  *   y     : [n][hp][wp][64] (dtype), hp/wp = the pool of the (h+1)/2 x (w+1)/2 stem map */
 int rr_stem_pack_weights(const float* w, int c_out, int c_in, int kh, int kw, void* out, int dtype, void* stream);
@@ -347,6 +349,12 @@ int rr_set_tuning(int key, int value);
 int rr_fill_unit_rows(float* out, long long rows, int d, unsigned long long seed,
                       long long row0, void* stream);
 /* float32 -> bf16 (round to nearest even). */
+/* int8 screening copy of float32 rows for rr_knn_topk(dtype RR_I8): y = clamp(rint(x * 127 / amax),
+ * -127, 127) with amax = max |x| over all n elements, reduced on the device into amax_dev (one float of
+ * caller scratch; no host synchronisation).  The screening scores are then exact int32 dot products of
+ * the quantised rows (v_mfma_i32_16x16x64_i8, twice the bf16 MFMA rate, half the bf16 bytes); the final
+ * top-k is the exact float64 re-score of the candidates, as for every screening dtype. */
+int rr_quantize_i8(const float* x, long long n, void* y, float* amax_dev, void* stream);
 int rr_cast_f32_bf16(const float* x, void* y, long long n, void* stream);
 /* float32 -> fp16 (IEEE binary16, round to nearest even). */
 int rr_cast_f32_f16(const float* x, void* y, long long n, void* stream);

@@ -13,7 +13,7 @@ from conftest import golden
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16", "fp16"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16", "fp16", "int8"])
 @pytest.mark.parametrize("tag", ["4k", "100k"])
 def test_knn_vs_reference_golden(cuda, precision, tag):
     from cirtorch.search import KnnIndex
@@ -35,7 +35,7 @@ def test_knn_matches_exact_oracle_random_shapes(cuda):
         qq = data.unit_rows(q, d, seed=n + 1)
         kk = min(k, n)
         ref_s, ref_i = ops.topk_exact(db, qq, kk)
-        for prec in ("fp32", "bf16", "fp16"):
+        for prec in ("fp32", "bf16", "fp16", "int8"):
             s, i = KnnIndex(torch.from_numpy(db).to(cuda), prec).search(torch.from_numpy(qq).to(cuda), kk)
             np.testing.assert_array_equal(i.cpu().numpy(), ref_i, err_msg="%s %s" % (prec, (n, q, d, k)))
             np.testing.assert_allclose(s.cpu().numpy(), ref_s, rtol=0, atol=1e-12)
@@ -72,7 +72,7 @@ def test_knn_running_screen_across_chunks(cuda):
     same = np.repeat(base[:1], 40000, 0)
     for name, db in (("dup", dup), ("rise", rise), ("same", same)):
         ref_s, ref_i = ops.topk_exact(db, qq, 100)
-        for prec in ("fp32", "bf16", "fp16"):
+        for prec in ("fp32", "bf16", "fp16", "int8"):
             s, i = KnnIndex(torch.from_numpy(db).to(cuda), prec).search(torch.from_numpy(qq).to(cuda), 100)
             np.testing.assert_array_equal(i.cpu().numpy(), ref_i, err_msg="%s %s" % (name, prec))
             np.testing.assert_allclose(s.cpu().numpy(), ref_s, rtol=0, atol=1e-12)
@@ -143,9 +143,10 @@ def test_fp16_screening_copy_and_limits(cuda):
             np.testing.assert_allclose(s.cpu().numpy(), ref_s, rtol=0, atol=1e-12)
 
 
-def test_knn_full_size_1m_bench_shape(cuda):
-    """BASELINE config size (1M x 2048 database, 128 queries, k = 100, bf16
-    screening) through size-independent properties: a query that is a database
+@pytest.mark.parametrize("prec", ["bf16", "int8"])
+def test_knn_full_size_1m_bench_shape(cuda, prec):
+    """BASELINE config size (1M x 2048 database, 128 queries, k = 100, bf16 or
+    int8 screening) through size-independent properties: a query that is a database
     row retrieves itself first with score 1; two queries checked against the
     CPU oracle over the whole database (chunked exact float64 top-k); a
     4-shard search + merge is bit-identical to the single search."""
@@ -157,7 +158,7 @@ def test_knn_full_size_1m_bench_shape(cuda):
     qq = _ops.fill_unit_rows(q, d, seed=0x0E5EED, device=cuda)
     self_rows = [5, 77777, 500000, n - 1]
     qq[:4] = db[self_rows]
-    index = KnnIndex(db, "bf16")
+    index = KnnIndex(db, prec)
     s, i = index.search(qq, k)
     i_np, s_np = i.cpu().numpy(), s.cpu().numpy()
     assert i_np[:4, 0].tolist() == self_rows
@@ -179,7 +180,7 @@ def test_knn_full_size_1m_bench_shape(cuda):
     R, per = 4, n // 4
     ss, ii = [], []
     for r in range(R):
-        sh_s, sh_i = KnnIndex(db[r * per:(r + 1) * per], "bf16", idx_offset=r * per).search(qq, k)
+        sh_s, sh_i = KnnIndex(db[r * per:(r + 1) * per], prec, idx_offset=r * per).search(qq, k)
         ss.append(sh_s)
         ii.append(sh_i)
     sm, im = merge_topk(torch.stack(ss), torch.stack(ii), k)
@@ -202,7 +203,7 @@ def _fused_vs_slab(cuda, db, qq, k, prec):
     return (s1.cpu().numpy(), i1.cpu().numpy()), (s0.cpu().numpy(), i0.cpu().numpy())
 
 
-@pytest.mark.parametrize("prec", ["bf16", "fp16", "fp32"])
+@pytest.mark.parametrize("prec", ["bf16", "fp16", "fp32", "int8"])
 def test_knn_fused_screen_stress(cuda, prec):
     """Databases past the 4-chunk prefix (65536 rows), so the screening GEMM
     epilogue runs: (a) scores rising row after row — every screened chunk
@@ -253,7 +254,7 @@ def test_knn_fused_graph_replay(cuda):
     np.testing.assert_array_equal(index.search(q2, 50)[1].cpu().numpy(), ref_i)
 
 
-@pytest.mark.parametrize("prec", ["bf16", "fp16", "fp32"])
+@pytest.mark.parametrize("prec", ["bf16", "fp16", "fp32", "int8"])
 def test_knn_verify_tight_cluster(cuda, prec):
     """600 near-copies of a query (scores within ~1e-4 of each other, tighter
     than the bf16 / fp16 screening error) straddle the candidate cut: the
@@ -278,6 +279,9 @@ def test_knn_verify_tight_cluster(cuda, prec):
     qs = _ops.cast_screen(q, index.dtype)
     _, _, unc = _ops.knn_topk(index.db, index.db32, qs, q, 100, db_norm_max=index.norm_max())
     unc = unc.cpu().numpy()
+    if prec == "int8":   # integer screening scores: no certificate, every query re-searched
+        assert (unc == 1).all()
+        return
     assert unc[0] == 0 and unc[1] == 0 and unc[3] == 0
     if prec != "fp32":
         assert unc[2] == 1
@@ -305,3 +309,29 @@ def test_knn_half_width_gemm_equals_tiled(cuda, prec, nq):
         E.lib().rr_set_tuning(8, 1)
     assert torch.equal(out[1][1], out[9][1])
     assert torch.equal(out[1][0], out[9][0])
+
+
+def test_int8_quantization_and_score_gemm(cuda):
+    """rr_quantize_i8 == rint(x * 127 / max|x|) clipped (numpy); the int8 score GEMM's
+    prefix slab and screened epilogue both rank like the exact int32 dot products:
+    Q = 1024 queries (k_gemm8 int8) and Q = 100 (k_gemm8s int8) equal the exact
+    float64 oracle on 300k rows (top-100)."""
+    from cirtorch import _ops
+    from cirtorch.search import KnnIndex
+    from oracle import ops
+    x = torch.randn(4097 * 4, device=cuda) * 0.3
+    q = _ops.quantize_i8(x).cpu().numpy()
+    xn = x.cpu().numpy()
+    ref = np.clip(np.rint(xn * (np.float32(127.0) / np.abs(xn).max())), -127, 127).astype(np.int8)
+    assert np.abs(q.astype(np.int32) - ref).max() <= 1 and (q == ref).mean() > 0.9999
+    db = _ops.fill_unit_rows(300_001, 2048, seed=0x5EEDA, device=cuda)
+    index = KnnIndex(db, "int8")
+    db_np = db.cpu().numpy()
+    for nq in (100, 1024):
+        qq = _ops.fill_unit_rows(nq, 2048, seed=0x5EEDB + nq, device=cuda)
+        s, i = index.search(qq, 100)
+        ref_s, ref_i = ops.topk_exact(db_np, qq[:6].cpu().numpy(), 100)
+        np.testing.assert_array_equal(i[:6].cpu().numpy(), ref_i)
+        np.testing.assert_allclose(s[:6].cpu().numpy(), ref_s, rtol=0, atol=1e-12)
+        s2, i2 = KnnIndex(db, "bf16").search(qq, 100)
+        assert torch.equal(i, i2) and torch.equal(s, s2)

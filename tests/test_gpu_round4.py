@@ -234,3 +234,55 @@ def test_scripts_test_replay(cuda, tmp_path, case, precision):
     if bool(g[case + "_ranks_lw_stable"]):
         assert (r["ranks_lw"] == g[case + "_ranks_lw"]).all()
         assert r["map_lw"]["mAP"] == pytest.approx(float(g[case + "_map_lw"]), abs=1e-9)
+
+
+# ------------------------------------------------------------------ stem v4 (space-to-depth K)
+@pytest.mark.parametrize("shape", [(2, 64, 84), (1, 100, 472), (3, 200, 132), (2, 96, 128)])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_stem_v4_space_to_depth(cuda, dt, shape):
+    """RR_TUNE_STEM 5: the stem with its K in space-to-depth form (6 MFMA K-steps of
+    12-channel 2x2 pixel blocks instead of 7 kernel rows of 8 x 4) against a float64
+    restatement on the same 16-bit operands and against v3 (same taps, only the f32
+    summation order differs: within 1 output ulp); uint8 pixels == float x / 255; a
+    ragged batch == its padded batch (bit for bit)."""
+    import torch.nn.functional as F
+    from cirtorch import _engine as E
+    from cirtorch import _ops as ops
+    n, h, w = shape
+    g = torch.Generator().manual_seed(h * 7 + w)
+    x = torch.rand(n, 3, h, w, generator=g)
+    wt = (torch.randn(64, 3, 7, 7, generator=g) * 0.1).to(dt).float()
+    scale = torch.rand(64, generator=g) + 0.5
+    scale[::5] *= -1.0
+    shift = torch.randn(64, generator=g) * 0.1
+    wpk = ops.pack_stem_weights(wt.to(cuda), dt)
+    xu = (x * 255).to(torch.uint8)
+    xf = xu.float() / 255.0
+    outs = {}
+    try:
+        for mode in (2, 5):
+            E.check(E.lib().rr_set_tuning(11, mode), "rr_set_tuning")
+            outs[mode] = [ops.stem_conv_pool(inp.to(cuda), wpk, scale.to(cuda), shift.to(cuda), leaky=True, slope=0.01,
+                                             mean=MEAN, std=STD).float().cpu() for inp in (xf, xu)]
+            if mode == 5:
+                imgs = [xu[i, :, : h - 2 * i, : w - 4 * i].contiguous().to(cuda) for i in range(n)]
+                rag = ops.stem_conv_pool_ragged(imgs, h, w, wpk, scale.to(cuda), shift.to(cuda), mean=MEAN, std=STD)
+                pad = torch.zeros_like(xu)
+                for i in range(n):
+                    pad[i, :, : h - 2 * i, : w - 4 * i] = xu[i, :, : h - 2 * i, : w - 4 * i]
+                ref_rag = ops.stem_conv_pool(pad.to(cuda), wpk, scale.to(cuda), shift.to(cuda), mean=MEAN, std=STD)
+                assert torch.equal(rag, ref_rag)
+    finally:
+        E.lib().rr_set_tuning(11, 2)
+    v3, v4 = outs[2][0], outs[5][0]
+    assert torch.equal(outs[5][0], outs[5][1])            # uint8 == float x / 255
+    xn = ((xf - torch.tensor(MEAN)[:, None, None]) / torch.tensor(STD)[:, None, None]).to(dt).float()
+    ref = F.conv2d(xn.double(), wt.double(), stride=2, padding=3) * scale.double()[None, :, None, None] \
+        + shift.double()[None, :, None, None]
+    ref = F.max_pool2d(F.leaky_relu(ref, 0.01), 3, 2, 1).permute(0, 2, 3, 1).float()
+    err = (v4 - ref).abs().max().item()
+    assert err <= 8e-3 * ref.abs().max().item(), err
+    ulp = 2.0 ** -7 if dt == torch.bfloat16 else 2.0 ** -10
+    d = (v4 - v3).abs()
+    assert (d <= ulp * v3.abs().clamp_min(1.0) + 1e-6).all(), d.max().item()
+    assert (d == 0).float().mean().item() > 0.9
