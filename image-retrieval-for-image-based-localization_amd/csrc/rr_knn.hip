@@ -276,10 +276,48 @@ __global__ void __launch_bounds__(SEL_THREADS) k_chunk_select(const float* __res
         uint4 kq[PER];
         int cnt[PER];
 #pragma unroll
+        for (int j = 0; j < PER; ++j) kq[j] = make_uint4(keep(v[j].x), keep(v[j].y), keep(v[j].z), keep(v[j].w));
+        // Pre-screen bound (KC <= 1024, KC % 16 == 0): every wave sorts its 64
+        // lane maxima (16 keys each) and takes the (KC/16)-th largest; the
+        // smallest of these 16 wave values m has KC distinct keys >= it (KC/16
+        // lane maxima per wave), so m <= the chunk's KC-th key and keys below
+        // it cannot be selected.  ~2-4 % of a chunk survives (vs all of it):
+        // the radix passes run over a compacted few hundred keys.
+        uint32_t m = 0u;
+        if (KC <= 1024 && (KC & 15) == 0) {
+            uint32_t lm = 0u;
+#pragma unroll
+            for (int j = 0; j < PER; ++j) lm = max(lm, max(max(kq[j].x, kq[j].y), max(kq[j].z, kq[j].w)));
+            // bitonic sort of the 64 lane maxima, descending
+#pragma unroll
+            for (int kb = 2; kb <= 64; kb <<= 1)
+#pragma unroll
+                for (int jb = kb >> 1; jb > 0; jb >>= 1) {
+                    const uint32_t o2 = (uint32_t)__shfl_xor((int)lm, jb, 64);
+                    const bool desc = (lane & kb) == 0, lower = (lane & jb) == 0;
+                    lm = (desc == lower) ? max(lm, o2) : min(lm, o2);
+                }
+            const uint32_t wm = (uint32_t)__shfl((int)lm, KC / 16 - 1, 64);
+            if (lane == 0) wcnt[w] = (int)wm;
+            __syncthreads();
+            m = 0xffffffffu;
+#pragma unroll
+            for (int j = 0; j < SEL_WAVES; ++j) m = min(m, (uint32_t)wcnt[j]);
+            __syncthreads();
+        }
+        mine = 0;
+#pragma unroll
         for (int j = 0; j < PER; ++j) {
-            const int m0 = mine;
-            kq[j] = make_uint4(keep(v[j].x), keep(v[j].y), keep(v[j].z), keep(v[j].w));
-            cnt[j] = mine - m0;
+            uint32_t kk[4] = {kq[j].x, kq[j].y, kq[j].z, kq[j].w};
+            int c2 = 0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                kk[e] = kk[e] >= m ? kk[e] : 0u;
+                c2 += kk[e] != 0u;
+            }
+            kq[j] = make_uint4(kk[0], kk[1], kk[2], kk[3]);
+            cnt[j] = c2;
+            mine += c2;
         }
 #pragma unroll
         for (int s2 = 32; s2 > 0; s2 >>= 1) mine += __shfl_xor(mine, s2, 64);
@@ -290,6 +328,37 @@ __global__ void __launch_bounds__(SEL_THREADS) k_chunk_select(const float* __res
         for (int j = 0; j < SEL_WAVES; ++j) {
             nvalid += wcnt[j];
             before += j < w ? wcnt[j] : 0;
+        }
+        if (nvalid > KC && nvalid <= CHUNK_L / 2) {
+            // compact the survivors into LDS in index order (keys | indices)
+            uint32_t* ck = keys;
+            int* ci = reinterpret_cast<int*>(keys + CHUNK_L / 2);
+            int run = before;
+#pragma unroll
+            for (int j = 0; j < PER; ++j) {
+                int x = cnt[j];
+#pragma unroll
+                for (int s2 = 1; s2 < 64; s2 <<= 1) {
+                    const int y = __shfl_up(x, s2, 64);
+                    if (lane >= s2) x += y;
+                }
+                int slot = run + x - cnt[j];
+                run += __shfl(x, 63, 64);
+                const uint32_t kk[4] = {kq[j].x, kq[j].y, kq[j].z, kq[j].w};
+                const int i0 = base + (w * 256 + j * 64 + lane) * 4;
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (kk[e] != 0u) {
+                        ck[slot] = kk[e];
+                        ci[slot] = i0 + e;
+                        ++slot;
+                    }
+            }
+            __syncthreads();
+            const uint32_t thr = block_topk([&](int i) { return ck[i]; }, [&](int i) { return ci[i]; }, nvalid, KC,
+                                            cand_k + o, cand_i + o, smi);
+            if (threadIdx.x == 0 && thr > tq) atomicMax(tau + q, thr);
+            return;
         }
         if (nvalid <= KC) {
             int run = before;

@@ -650,6 +650,176 @@ __global__ void __launch_bounds__(512, 1) k_pair_mid(PairMidArgs a) {
 }
 
 
+// ---------------------------------------------------------------------------
+// Weight-stationary residual 1x1 (the bottleneck conv3 of mod4 / mod5:
+// 256 -> 1024 and 512 -> 2048, BN, + residual, activation).
+// k_stream1x1 keeps the weight slice in LDS and streams the activations into
+// VGPRs, so every MFMA re-reads a 1 KiB A fragment from LDS: at K = 512 the
+// LDS port, not the matrix cores, sets its pace (~600 TFLOP/s).  Here the
+// roles flip:
+//   * each wave holds its CW output channels x all K of the PERM32 weights in
+//     VGPRs for the whole launch (CW / 16 x K / 32 fragments = 128 VGPRs);
+//     a block (8 waves, one per CU, persistent) owns BC = 8 CW channels;
+//   * activation tiles [TP pixels][K] and the residual tile [TP][BC] arrive
+//     by LDS-DMA into one of three buffers, two tiles ahead (~100 KiB in
+//     flight per CU), swizzled (16-B chunk XOR pixel & 15) on the source side;
+//   * a B fragment read from LDS feeds CW / 16 MFMAs (4 at K = 256, 2 at
+//     K = 512, vs 1 in k_stream1x1); the residual is read from LDS in the
+//     epilogue.
+// The nslices channel slices of one pixel tile run on one XCD (block b of
+// the XCD-contiguous map), so the activation tile is fetched from HBM once
+// and re-read from that XCD's L2.  MFMA accumulation order per element
+// (K-steps 0..K/32-1 from zero) equals k_stream1x1's: outputs are
+// bit-identical to it.
+struct WresArgs {
+    const bf16_t* x;    // [P][K]
+    const bf16_t* w;    // [C][K] PERM32 rows
+    const float *scale, *shift;
+    const bf16_t* res;  // [P][ldy]
+    bf16_t* y;          // [P][ldy]
+    long long P;
+    int ldy, nslices, xmap, act;
+    float slope;
+};
+
+template <int K, int CW, typename H>
+__global__ void __launch_bounds__(512, 1) k_wres1x1(WresArgs a) {
+    constexpr int TP = 32, NJ = TP / 16, NI = CW / 16, NK = K / 32, BC = 8 * CW;
+    constexpr int XRB = K * 2, RRB = BC * 2;          // row bytes of the two tiles
+    constexpr int XB = TP * XRB, RB = TP * RRB;       // tile bytes
+    constexpr int BUF = XB + RB, NBUF = 3;
+    constexpr int NDX = XB / 1024 / 8, NDR = RB / 1024 / 8;  // DMA instructions per wave
+    constexpr int ND = NDX + NDR, NST = (CW / 32) * NJ;      // ... and stores per wave per tile
+    static_assert(NI * NK == 32 && XB % 8192 == 0 && RB % 8192 == 0, "tile shape");
+    static_assert(XRB <= 1024 && RRB <= 1024, "row fits one DMA instruction");
+    __shared__ __attribute__((aligned(1024))) char smem[NBUF * BUF];
+    __shared__ __attribute__((aligned(16))) float sS[BC], sH[BC];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r16 = lane & 15, kq = lane >> 4;
+    const int b = (int)blockIdx.x, ns = a.nslices;
+    const int slice = a.xmap ? (b >> 3) % ns : b % ns;
+    const int bi = a.xmap ? ((b >> 3) / ns) * 8 + (b & 7) : b / ns;
+    const int G = (int)gridDim.x / ns;
+    const int c0 = slice * BC, cw0 = c0 + CW * wave;
+
+    const bool affine = a.scale != nullptr;
+    for (int i = tid; i < BC; i += 512) {
+        sS[i] = affine ? a.scale[c0 + i] : 1.f;
+        sH[i] = affine ? a.shift[c0 + i] : 0.f;
+    }
+    uint4 areg[NI][NK];
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int kk = 0; kk < NK; ++kk)
+            areg[i][kk] = *reinterpret_cast<const uint4*>(a.w + (long long)(cw0 + 16 * i + r16) * K + 32 * kk + 8 * kq);
+    __syncthreads();
+
+    const long long P = a.P;
+    const int ntiles = (int)((P + TP - 1) / TP);
+    if (bi >= ntiles) return;
+    const si32x4_t rsX = srsrc(a.x, (unsigned)(P * XRB));
+    const si32x4_t rsR = srsrc(a.res + c0, (unsigned)(P * a.ldy * 2 - (long long)c0 * 2));
+    const unsigned lds0 = (unsigned)(unsigned long long)smem;
+    // instruction d of a tile moves LDS bytes [1 KiB d, 1 KiB (d + 1)): 1024 / row-bytes pixels
+    auto dma = [&](int t, int buf) {
+#pragma unroll
+        for (int u = 0; u < NDX; ++u) {
+            constexpr int CPR = XRB / 16;
+            const int d = NDX * wave + u, px = d * (1024 / XRB) + lane / CPR, slot = lane % CPR;
+            const unsigned off = (unsigned)(((long long)t * TP + px) * XRB) + (unsigned)((slot ^ (px & 15)) << 4);
+            sdma16(rsX, off, lds0 + buf * BUF + d * 1024);
+        }
+#pragma unroll
+        for (int u = 0; u < NDR; ++u) {
+            constexpr int CPR = RRB / 16;
+            const int d = NDR * wave + u, px = d * (1024 / RRB) + lane / CPR, slot = lane % CPR;
+            const unsigned off = (unsigned)(((long long)t * TP + px) * a.ldy * 2) + (unsigned)((slot ^ (px & 15)) << 4);
+            sdma16(rsR, off, lds0 + buf * BUF + XB + d * 1024);
+        }
+    };
+    const bool leaky = a.act == RR_ACT_LEAKY;
+
+    dma(bi, 0);
+    if (bi + G < ntiles) dma(bi + G, 1);
+    for (int k = 0, t = bi; t < ntiles; ++k, t += G) {
+        const int cur = k % NBUF;
+        // tile t's DMA landed: still in flight after it may be tile t + G's DMA and
+        // (k > 0) this wave's stores of tile t - G, issued in that order
+        if (t + G < ntiles) {
+            if (k == 0) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(ND) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(ND + NST) : "memory");
+        } else {
+            if (k == 0) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(NST) : "memory");
+        }
+        // every wave is past tile t - G: its buffer takes tile t + 2G
+        if (t + 2 * G < ntiles) dma(t + 2 * G, (k + 2) % NBUF);
+        const char* X = smem + cur * BUF;
+        const char* Rt = X + XB;
+        h16_f32x4_t acc[NI][NJ];
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) acc[i][j] = (h16_f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < NK; ++kk) {
+            uint4 bx[NJ];
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int px = 16 * j + r16;
+                bx[j] = *reinterpret_cast<const uint4*>(X + px * XRB + (((4 * kk + kq) ^ (px & 15)) << 4));
+            }
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) acc[i][j] = H16<H>::mfma(areg[i][kk], bx[j], acc[i][j]);
+        }
+#pragma unroll
+        for (int i2 = 0; i2 < CW / 32; ++i2) {
+            const int cl = CW * wave + 32 * i2 + 8 * kq;  // 8 consecutive channels of this lane (PERM32)
+            const float4 sc0 = *reinterpret_cast<const float4*>(sS + cl);
+            const float4 sc1 = *reinterpret_cast<const float4*>(sS + cl + 4);
+            const float4 sh0 = *reinterpret_cast<const float4*>(sH + cl);
+            const float4 sh1 = *reinterpret_cast<const float4*>(sH + cl + 4);
+            const float sc[8] = {sc0.x, sc0.y, sc0.z, sc0.w, sc1.x, sc1.y, sc1.z, sc1.w};
+            const float sh[8] = {sh0.x, sh0.y, sh0.z, sh0.w, sh1.x, sh1.y, sh1.z, sh1.w};
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int px = 16 * j + r16;
+                const uint4 q = *reinterpret_cast<const uint4*>(Rt + px * RRB + (((cl >> 3) ^ (px & 15)) << 4));
+                const unsigned w4[4] = {q.x, q.y, q.z, q.w};
+                float v[8];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    v[r] = acc[2 * i2][j][r] * sc[r] + sh[r];
+                    v[4 + r] = acc[2 * i2 + 1][j][r] * sc[4 + r] + sh[4 + r];
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    v[2 * r] += H16<H>::lo(w4[r]);
+                    v[2 * r + 1] += H16<H>::hi(w4[r]);
+                }
+                if (leaky) {
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * a.slope;
+                }
+                uint4 o;
+                o.x = H16<H>::pack2(v[0], v[1]);
+                o.y = H16<H>::pack2(v[2], v[3]);
+                o.z = H16<H>::pack2(v[4], v[5]);
+                o.w = H16<H>::pack2(v[6], v[7]);
+                const long long p = (long long)t * TP + px;
+                if (p < P) st16_once(a.y + p * a.ldy + c0 + cl, o);
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+
 }  // namespace
 int g_stream_xcd = 1;  // rr_set_tuning(RR_TUNE_STREAM_XCD): channel slices of one strip on one XCD
 namespace {
@@ -676,6 +846,40 @@ void launch_s_t(const ConvArgs& a, hipStream_t s) {
 }  // namespace
 
 int g_stream_mode = 1;  // rr_set_tuning(RR_TUNE_STREAM_1X1): 0 off, 1 auto, 2 / 3 see launch_stream1x1
+int g_wres = 0;         // rr_set_tuning(RR_TUNE_WRES)
+
+namespace {
+template <int K, int CW>
+void launch_wres(const ConvArgs& a, hipStream_t s, bool f16) {
+    constexpr int TP = 32, BC = 8 * CW;
+    WresArgs w;
+    w.w = (const bf16_t*)a.w;
+    const bool affine = a.flags & RR_CONV_AFFINE;
+    w.scale = affine ? a.scale : nullptr;
+    w.shift = affine ? a.shift : nullptr;
+    w.ldy = a.ldy;
+    w.act = a.act;
+    w.slope = a.slope;
+    w.nslices = a.cout / BC;
+    int per = grid_cus() / w.nslices;
+    if (per < 1) per = 1;
+    // pixel chunks whose residual / output rows stay inside 31-bit buffer offsets
+    const long long CH = ((1ll << 31) / ((long long)a.ldy * 2 + K * 2)) / TP * TP;
+    for (long long p0 = 0; p0 < a.P; p0 += CH) {
+        const long long pn = a.P - p0 < CH ? a.P - p0 : CH;
+        w.x = (const bf16_t*)a.x + p0 * K;
+        w.res = (const bf16_t*)a.res + p0 * a.ldy;
+        w.y = (bf16_t*)a.y + p0 * a.ldy;
+        w.P = pn;
+        const long long ntiles = (pn + TP - 1) / TP;
+        const int ps = (int)(per < ntiles ? per : ntiles);
+        const int grid = ps * w.nslices;
+        w.xmap = w.nslices > 1 && grid % (8 * w.nslices) == 0;
+        if (f16) hipLaunchKernelGGL((k_wres1x1<K, CW, f16_t>), dim3(grid), dim3(512), 0, s, w);
+        else hipLaunchKernelGGL((k_wres1x1<K, CW, bf16_t>), dim3(grid), dim3(512), 0, s, w);
+    }
+}
+}  // namespace
 
 // bf16 1x1 (pad 0, any stride), PERM32 weights, bf16 out: returns false when the
 // shape is not one the streaming kernel is built for (caller uses the tiled engine).
@@ -693,6 +897,10 @@ bool launch_stream1x1(const ConvArgs& a, hipStream_t s, bool f16) {
     if (a.P < 4096 || (long long)a.n * a.h * a.w_ * a.cin >= (1ll << 31)) return false;
     const bool res = a.flags & RR_CONV_RESIDUAL;
     const int K = a.cin, C = a.cout;
+    if (g_wres && res && a.stride == 1 && a.h == a.ho && a.w_ == a.wo && (a.ldy & 7) == 0) {
+        if (K == 512 && C == 2048) { launch_wres<512, 32>(a, s, f16); return true; }
+        if (K == 256 && C == 1024) { launch_wres<256, 64>(a, s, f16); return true; }
+    }
     // mode 2: the residual 512 -> 2048 1x1 (mod5 conv3) on the 8-phase GEMM;
     // mode 3: also the residual 256 -> 1024 1x1 (mod4 conv3)
     if (g_stream_mode >= 2 && K == 512 && C == 2048 && res && gemm8_eligible(a, true, 2)) return false;

@@ -128,6 +128,31 @@ def test_stream1x1_xcd_map(cuda, case):
     assert torch.equal(outs[0], outs[1])
 
 
+WRES_CASES = [
+    # residual conv3 shapes of mod4 / mod5 that k_wres1x1 takes (RR_TUNE_WRES = 1)
+    (1, 256, 65, 67, 1024, 1, 1, 0, True, True),    # 4355 pixels: partial last tile, 2 slices
+    (1, 512, 64, 67, 2048, 1, 1, 0, True, True),    # 8 slices of 256 channels
+    (4, 256, 48, 64, 1024, 1, 1, 0, True, True),    # chip-filling grid: XCD map on
+    (2, 512, 48, 64, 2048, 1, 1, 0, True, False),   # identity activation
+]
+
+
+@pytest.mark.parametrize("case", WRES_CASES)
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_wres1x1(cuda, case, prec):
+    """Weight-stationary residual 1x1 (weights in VGPRs, tiles by LDS-DMA):
+    exact vs float64 and bit-identical to the streaming 1x1 (same K order)."""
+    from cirtorch import _engine as E
+    outs = []
+    try:
+        for on in (1, 0):
+            E.check(E.lib().rr_set_tuning(14, on), "rr_set_tuning")
+            outs.append(_check_conv(cuda, case, prec, True))
+    finally:
+        E.lib().rr_set_tuning(14, 0)
+    assert torch.equal(outs[0], outs[1])
+
+
 CONV3_CASES = [
     # bf16 stride-1 3x3 shapes the direct LDS-patch kernel (rr_conv3.hip) takes
     (2, 64, 16, 64, 64, 3, 1, 1, False, True),     # c_in = c_out = 64: weights resident in LDS
