@@ -438,6 +438,146 @@ __global__ void __launch_bounds__(64 * WC * WP) k_conv3x3(ConvArgs a, int tiles_
     }
 }
 
+// ---------------------------------------------------------------------------
+// mod2 3x3 (c_in = c_out = 64) with the weights in VGPRs.  k_conv3x3's
+// A-stationary form reads both operands from LDS: per MFMA 0.75 KiB (2 A + 4 B
+// fragments per 8 MFMAs), 1.5x what the LDS port delivers at the MFMA rate, and
+// the 72 KiB weight image leaves room for only two halo patches.  Here each
+// wave keeps its 32 output channels x all 576 K of the PERM32 weights in VGPRs
+// (2 x 18 fragments, 144 VGPRs) for the whole launch, so a B fragment read from
+// LDS feeds 2 MFMAs and nothing else is read; the LDS holds three 8x32-tile
+// halo patches (48 KiB each), prefetched two tiles ahead by LDS-DMA.
+// Persistent block per CU, 8 waves = 2 channel halves x 4 pixel quarters;
+// tiles walked XCD-contiguously (the 32 tiles an XCD holds at once are 4 tile
+// rows of one image: vertical halo re-reads hit its L2).  Accumulation order
+// (tap, half-step) equals k_conv3x3's: bit-identical outputs.
+template <typename HT>
+__global__ void __launch_bounds__(512, 1) k_c3w64(ConvArgs a, int tiles_w, int tiles_hw, int ntiles) {
+    constexpr int TH = 8, TW = 32, TP = TH * TW, PC = TW + 2, NPIX = (TH + 2) * PC;  // 340 patch pixels
+    constexpr int NDW = 6, PBYTES = 8 * NDW * 1024;  // patch: 48 wave-instructions of 8 pixels x 128 B
+    constexpr int NBUF = 3, FN = TP / 4 / 16, NST = FN;  // per wave: 4 pixel fragments, 4 epilogue stores
+    static_assert(8 * NDW * 8 >= NPIX, "patch pieces");
+    __shared__ __attribute__((aligned(1024))) char smem[NBUF * PBYTES];
+    __shared__ __attribute__((aligned(16))) float sS[64], sH[64];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wc = wave & 1, wp = wave >> 1;
+    const int r16 = lane & 15, kq = lane >> 4, lrow = lane >> 3, lch = lane & 7;
+    const int H = a.h, W = a.w_;
+    if (tid < 64) {
+        const bool aff = a.flags & RR_CONV_AFFINE;
+        sS[tid] = aff ? a.scale[tid] : 1.f;
+        sH[tid] = aff ? a.shift[tid] : 0.f;
+    }
+    uint4 areg[2][18];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int s = 0; s < 18; ++s)
+            areg[i][s] = *reinterpret_cast<const uint4*>((const bf16_t*)a.w + (long long)(32 * wc + 16 * i + r16) * 576 +
+                                                         (s >> 1) * 64 + 32 * (s & 1) + 8 * kq);
+    __syncthreads();
+
+    // XCD-contiguous walk: round i, XCD x = b & 7 takes tiles [i G + x G/8, ... + G/8)
+    const int b = (int)blockIdx.x, G = (int)gridDim.x;
+    auto tile_id = [&](int i) { return i * G + (b & 7) * (G >> 3) + (b >> 3); };
+    const pi32x4_t rsX = prsrc(a.x, (unsigned)((long long)a.n * H * W * 64 * 2));
+    const unsigned lds0 = (unsigned)(unsigned long long)smem;
+    auto patch_dma = [&](int t, int buf) {
+        const int img = t / tiles_hw, rem = t - img * tiles_hw, th = rem / tiles_w;
+        const int oh0 = th * TH, ow0 = (rem - th * tiles_w) * TW;
+#pragma unroll
+        for (int u = 0; u < NDW; ++u) {
+            const int d = NDW * wave + u, q = d * 8 + lrow;
+            const int pr = q / PC, pc = q - pr * PC;
+            const int hh = oh0 - 1 + pr, ww = ow0 - 1 + pc;
+            unsigned off = POOB;
+            if (t < ntiles && q < NPIX && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W)
+                off = (unsigned)(((((long long)img * H + hh) * W + ww) * 64 + ((lch ^ lrow) << 3)) * 2);
+            pdma16(rsX, off, lds0 + buf * PBYTES + d * 1024);
+        }
+    };
+    int bq[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+        const int p = wp * (TP / 4) + j * 16;
+        bq[j] = (p / TW) * PC + (p % TW) + r16;
+    }
+    bf16_t* __restrict__ Y = (bf16_t*)a.y;
+    const bool leaky = a.act == RR_ACT_LEAKY;
+    const float slope = a.slope;
+    const int nmine = (ntiles - 1 - (b >> 3) - (b & 7) * (G >> 3)) >= 0
+                          ? (ntiles - 1 - (b & 7) * (G >> 3) - (b >> 3)) / G + 1 : 0;
+    if (nmine == 0) return;
+    // every wave issues exactly NDW pieces per patch (pieces past the patch write
+    // zeros into the buffer's tail), so the counted waits below are uniform
+    patch_dma(tile_id(0), 0);
+    patch_dma(tile_id(1), 1);
+    for (int i = 0; i < nmine; ++i) {
+        // patch(i) landed: younger are patch(i + 1) and tile i - 1's stores
+        if (i == 0) pwait_barrier<NDW>();
+        else pwait_barrier<NDW + NST>();
+        patch_dma(tile_id(i + 2), (i + 2) % NBUF);
+        const char* Ps = smem + (i % NBUF) * PBYTES;
+        int bql[FN];
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+            bql[j] = bq[j];
+            asm volatile("" : "+v"(bql[j]));
+        }
+        pf32x4_t acc[2][FN];
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) acc[ii][j] = (pf32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 18; ++s) {
+            const int tap = s >> 1, ch = kq + 4 * (s & 1), toff = (tap / 3) * PC + tap % 3;
+            uint4 fb[FN];
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+                const int q = bql[j] + toff;
+                fb[j] = *reinterpret_cast<const uint4*>(Ps + q * 128 + ((ch ^ (q & 7)) << 4));
+            }
+#pragma unroll
+            for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+                for (int j = 0; j < FN; ++j) acc[ii][j] = H16<HT>::mfma(areg[ii][s], fb[j], acc[ii][j]);
+        }
+        const int t = tile_id(i);
+        const int img = t / tiles_hw, rem = t - img * tiles_hw, th = rem / tiles_w;
+        const int oh0 = th * TH, ow0 = (rem - th * tiles_w) * TW;
+        const int c = 32 * wc + 8 * kq;
+        const float4 s0 = *reinterpret_cast<const float4*>(sS + c), s1 = *reinterpret_cast<const float4*>(sS + c + 4);
+        const float4 h0 = *reinterpret_cast<const float4*>(sH + c), h1 = *reinterpret_cast<const float4*>(sH + c + 4);
+        const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+        const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+            const int p = wp * (TP / 4) + j * 16 + r16;
+            const long long pix = ((long long)img * H + oh0 + p / TW) * W + ow0 + p % TW;
+            float v[8];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                v[r] = acc[0][j][r] * sc[r] + sh[r];
+                v[4 + r] = acc[1][j][r] * sc[4 + r] + sh[4 + r];
+            }
+            if (leaky) {
+#pragma unroll
+                for (int r = 0; r < 8; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * slope;
+            }
+            uint4 o;
+            o.x = H16<HT>::pack2(v[0], v[1]);
+            o.y = H16<HT>::pack2(v[2], v[3]);
+            o.z = H16<HT>::pack2(v[4], v[5]);
+            o.w = H16<HT>::pack2(v[6], v[7]);
+            *reinterpret_cast<uint4*>(Y + pix * a.ldy + c) = o;
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 }  // namespace
 int g_conv3_pipe = 1;  // rr_set_tuning(RR_TUNE_CONV3_PIPE): 1 software-pipelined A-stationary tiles, 0 compiler schedule
 namespace {
@@ -460,6 +600,7 @@ void launch_c3(const ConvArgs& a, hipStream_t s, bool f16) {
 
 }  // namespace
 
+int g_c3w64 = 0;       // mod2 3x3 on k_c3w64 under RR_TUNE_CONV3X3 = 1 (9 forces it)
 int g_conv3_mode = 1;  // rr_set_tuning(RR_TUNE_CONV3X3): 0 off, 1 auto, 2 / 3 prefer 8x32 / 4x32 tiles,
                        // 4 / 6 A-stationary with 1x8 / 1x4 waves (auto: 2x4), 7 3-stage weight ring,
                        // 8 256-channel x 6x32 tiles (auto where c_out % 256 == 0 and h % 6 == 0)
@@ -484,6 +625,15 @@ bool launch_conv3x3(const ConvArgs& a, hipStream_t s, bool f16) {
     // kernel (420 vs 479, 392 vs 455 us) — the taps re-read from L2
     if (a.cout % 256 == 0 && g_conv3_mode == 1 && gemm8_eligible(a, false, 2)) return false;
     const int g_c3_cus = grid_cus();
+    if (a.cin == 64 && a.cout == 64 && a.h % 8 == 0 && (g_conv3_mode == 9 || (g_conv3_mode == 1 && g_c3w64))) {
+        const int tiles_w = a.w_ / 32, tiles_hw = tiles_w * (a.h / 8);
+        const long long ntl = (long long)a.n * tiles_hw;
+        int grid = (int)(ntl < g_c3_cus ? ntl : g_c3_cus) & ~7;
+        if (grid < 8) grid = 8;
+        if (f16) hipLaunchKernelGGL(k_c3w64<f16_t>, dim3(grid), dim3(512), 0, s, a, tiles_w, tiles_hw, (int)ntl);
+        else hipLaunchKernelGGL(k_c3w64<bf16_t>, dim3(grid), dim3(512), 0, s, a, tiles_w, tiles_hw, (int)ntl);
+        return true;
+    }
     if (a.cin == 64 && a.cout == 64 && a.h % 8 == 0) {
         // 8 waves (2 per SIMD) measured fastest: 125 us vs 146 (4 waves) at 32 x 192x256x64
         if (g_conv3_mode == 4) launch_c3<64, 8, 32, 1, 8, true>(a, s, f16);

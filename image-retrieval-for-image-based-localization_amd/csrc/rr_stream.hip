@@ -651,8 +651,10 @@ __global__ void __launch_bounds__(512, 1) k_pair_mid(PairMidArgs a) {
 
 
 // ---------------------------------------------------------------------------
-// Weight-stationary residual 1x1 (the bottleneck conv3 of mod4 / mod5:
-// 256 -> 1024 and 512 -> 2048, BN, + residual, activation).
+// Weight-stationary 1x1 with the weights in VGPRs (the bottleneck conv3 of
+// mod4 / mod5: 256 -> 1024 and 512 -> 2048, BN, + residual, activation; the
+// K = 256 / 512 projections and the mod4 block-1 conv1, without residual,
+// strided or not).
 // k_stream1x1 keeps the weight slice in LDS and streams the activations into
 // VGPRs, so every MFMA re-reads a 1 KiB A fragment from LDS: at K = 512 the
 // LDS port, not the matrix cores, sets its pace (~600 TFLOP/s).  Here the
@@ -660,9 +662,10 @@ __global__ void __launch_bounds__(512, 1) k_pair_mid(PairMidArgs a) {
 //   * each wave holds its CW output channels x all K of the PERM32 weights in
 //     VGPRs for the whole launch (CW / 16 x K / 32 fragments = 128 VGPRs);
 //     a block (8 waves, one per CU, persistent) owns BC = 8 CW channels;
-//   * activation tiles [TP pixels][K] and the residual tile [TP][BC] arrive
-//     by LDS-DMA into one of three buffers, two tiles ahead (~100 KiB in
-//     flight per CU), swizzled (16-B chunk XOR pixel & 15) on the source side;
+//   * activation tiles [TP pixels][K] (RES: and the residual tile [TP][BC])
+//     arrive by LDS-DMA into one of three buffers, two tiles ahead (~100 KiB
+//     in flight per CU), swizzled (16-B chunk XOR pixel & 15) on the source
+//     side; a strided conv gathers its input rows in the DMA offsets;
 //   * a B fragment read from LDS feeds CW / 16 MFMAs (4 at K = 256, 2 at
 //     K = 512, vs 1 in k_stream1x1); the residual is read from LDS in the
 //     epilogue.
@@ -672,21 +675,22 @@ __global__ void __launch_bounds__(512, 1) k_pair_mid(PairMidArgs a) {
 // (K-steps 0..K/32-1 from zero) equals k_stream1x1's: outputs are
 // bit-identical to it.
 struct WresArgs {
-    const bf16_t* x;    // [P][K]
+    const bf16_t* x;    // [n][h][w][K]
     const bf16_t* w;    // [C][K] PERM32 rows
     const float *scale, *shift;
-    const bf16_t* res;  // [P][ldy]
+    const bf16_t* res;  // [P][ldy] (RES)
     bf16_t* y;          // [P][ldy]
     long long P;
     int ldy, nslices, xmap, act;
     float slope;
+    int h, w_, ho, wo, stride;
 };
 
-template <int K, int CW, typename H>
+template <int K, int CW, bool RES, typename H>
 __global__ void __launch_bounds__(512, 1) k_wres1x1(WresArgs a) {
     constexpr int TP = 32, NJ = TP / 16, NI = CW / 16, NK = K / 32, BC = 8 * CW;
-    constexpr int XRB = K * 2, RRB = BC * 2;          // row bytes of the two tiles
-    constexpr int XB = TP * XRB, RB = TP * RRB;       // tile bytes
+    constexpr int XRB = K * 2, RRB = RES ? BC * 2 : 0;  // row bytes of the two tiles
+    constexpr int XB = TP * XRB, RB = TP * RRB;         // tile bytes
     constexpr int BUF = XB + RB, NBUF = 3;
     constexpr int NDX = XB / 1024 / 8, NDR = RB / 1024 / 8;  // DMA instructions per wave
     constexpr int ND = NDX + NDR, NST = (CW / 32) * NJ;      // ... and stores per wave per tile
@@ -720,24 +724,35 @@ __global__ void __launch_bounds__(512, 1) k_wres1x1(WresArgs a) {
     const long long P = a.P;
     const int ntiles = (int)((P + TP - 1) / TP);
     if (bi >= ntiles) return;
-    const si32x4_t rsX = srsrc(a.x, (unsigned)(P * XRB));
-    const si32x4_t rsR = srsrc(a.res + c0, (unsigned)(P * a.ldy * 2 - (long long)c0 * 2));
+    const long long nimg = P / ((long long)a.ho * a.wo);
+    const si32x4_t rsX = srsrc(a.x, (unsigned)(nimg * a.h * a.w_ * XRB));
+    si32x4_t rsR = rsX;
+    if constexpr (RES) rsR = srsrc(a.res + c0, (unsigned)(P * a.ldy * 2 - (long long)c0 * 2));
     const unsigned lds0 = (unsigned)(unsigned long long)smem;
+    const int hw = a.ho * a.wo;
+    auto x_row = [&](unsigned p) -> unsigned {  // input row of output pixel p (past the end: past the buffer)
+        if (a.stride == 1) return p;
+        const unsigned img = p / (unsigned)hw, rem = p - img * (unsigned)hw;
+        const unsigned oh = rem / (unsigned)a.wo, ow = rem - oh * (unsigned)a.wo;
+        return (img * (unsigned)a.h + oh * (unsigned)a.stride) * (unsigned)a.w_ + ow * (unsigned)a.stride;
+    };
     // instruction d of a tile moves LDS bytes [1 KiB d, 1 KiB (d + 1)): 1024 / row-bytes pixels
     auto dma = [&](int t, int buf) {
 #pragma unroll
         for (int u = 0; u < NDX; ++u) {
             constexpr int CPR = XRB / 16;
             const int d = NDX * wave + u, px = d * (1024 / XRB) + lane / CPR, slot = lane % CPR;
-            const unsigned off = (unsigned)(((long long)t * TP + px) * XRB) + (unsigned)((slot ^ (px & 15)) << 4);
+            const unsigned off = x_row((unsigned)(t * TP + px)) * XRB + (unsigned)((slot ^ (px & 15)) << 4);
             sdma16(rsX, off, lds0 + buf * BUF + d * 1024);
         }
+        if constexpr (RES) {
 #pragma unroll
-        for (int u = 0; u < NDR; ++u) {
-            constexpr int CPR = RRB / 16;
-            const int d = NDR * wave + u, px = d * (1024 / RRB) + lane / CPR, slot = lane % CPR;
-            const unsigned off = (unsigned)(((long long)t * TP + px) * a.ldy * 2) + (unsigned)((slot ^ (px & 15)) << 4);
-            sdma16(rsR, off, lds0 + buf * BUF + XB + d * 1024);
+            for (int u = 0; u < NDR; ++u) {
+                constexpr int CPR = RRB / 16;
+                const int d = NDR * wave + u, px = d * (1024 / RRB) + lane / CPR, slot = lane % CPR;
+                const unsigned off = (unsigned)(((long long)t * TP + px) * a.ldy * 2) + (unsigned)((slot ^ (px & 15)) << 4);
+                sdma16(rsR, off, lds0 + buf * BUF + XB + d * 1024);
+            }
         }
     };
     const bool leaky = a.act == RR_ACT_LEAKY;
@@ -789,18 +804,20 @@ __global__ void __launch_bounds__(512, 1) k_wres1x1(WresArgs a) {
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
                 const int px = 16 * j + r16;
-                const uint4 q = *reinterpret_cast<const uint4*>(Rt + px * RRB + (((cl >> 3) ^ (px & 15)) << 4));
-                const unsigned w4[4] = {q.x, q.y, q.z, q.w};
                 float v[8];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     v[r] = acc[2 * i2][j][r] * sc[r] + sh[r];
                     v[4 + r] = acc[2 * i2 + 1][j][r] * sc[4 + r] + sh[4 + r];
                 }
+                if constexpr (RES) {
+                    const uint4 q = *reinterpret_cast<const uint4*>(Rt + px * RRB + (((cl >> 3) ^ (px & 15)) << 4));
+                    const unsigned w4[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    v[2 * r] += H16<H>::lo(w4[r]);
-                    v[2 * r + 1] += H16<H>::hi(w4[r]);
+                    for (int r = 0; r < 4; ++r) {
+                        v[2 * r] += H16<H>::lo(w4[r]);
+                        v[2 * r + 1] += H16<H>::hi(w4[r]);
+                    }
                 }
                 if (leaky) {
 #pragma unroll
@@ -851,7 +868,8 @@ int g_wres = 0;         // rr_set_tuning(RR_TUNE_WRES)
 namespace {
 template <int K, int CW>
 void launch_wres(const ConvArgs& a, hipStream_t s, bool f16) {
-    constexpr int TP = 32, BC = 8 * CW;
+    constexpr int BC = 8 * CW;
+    const bool res = a.flags & RR_CONV_RESIDUAL;
     WresArgs w;
     w.w = (const bf16_t*)a.w;
     const bool affine = a.flags & RR_CONV_AFFINE;
@@ -860,23 +878,32 @@ void launch_wres(const ConvArgs& a, hipStream_t s, bool f16) {
     w.ldy = a.ldy;
     w.act = a.act;
     w.slope = a.slope;
+    w.h = a.h; w.w_ = a.w_; w.ho = a.ho; w.wo = a.wo; w.stride = a.stride;
     w.nslices = a.cout / BC;
     int per = grid_cus() / w.nslices;
     if (per < 1) per = 1;
-    // pixel chunks whose residual / output rows stay inside 31-bit buffer offsets
-    const long long CH = ((1ll << 31) / ((long long)a.ldy * 2 + K * 2)) / TP * TP;
-    for (long long p0 = 0; p0 < a.P; p0 += CH) {
-        const long long pn = a.P - p0 < CH ? a.P - p0 : CH;
-        w.x = (const bf16_t*)a.x + p0 * K;
-        w.res = (const bf16_t*)a.res + p0 * a.ldy;
-        w.y = (bf16_t*)a.y + p0 * a.ldy;
-        w.P = pn;
-        const long long ntiles = (pn + TP - 1) / TP;
+    // whole-image chunks whose input and residual / output stay inside 31-bit buffer offsets
+    const long long in_img = (long long)a.h * a.w_ * K * 2, out_img = (long long)a.ho * a.wo * a.ldy * 2;
+    long long ich = (1ll << 31) / (in_img > out_img ? in_img : out_img);
+    if (ich < 1) ich = 1;
+    const long long hw = (long long)a.ho * a.wo;
+    for (long long i0 = 0; i0 < a.n; i0 += ich) {
+        const long long ni = a.n - i0 < ich ? a.n - i0 : ich;
+        w.x = (const bf16_t*)a.x + i0 * a.h * a.w_ * K;
+        w.res = res ? (const bf16_t*)a.res + i0 * hw * a.ldy : nullptr;
+        w.y = (bf16_t*)a.y + i0 * hw * a.ldy;
+        w.P = ni * hw;
+        const long long ntiles = (w.P + 31) / 32;
         const int ps = (int)(per < ntiles ? per : ntiles);
         const int grid = ps * w.nslices;
         w.xmap = w.nslices > 1 && grid % (8 * w.nslices) == 0;
-        if (f16) hipLaunchKernelGGL((k_wres1x1<K, CW, f16_t>), dim3(grid), dim3(512), 0, s, w);
-        else hipLaunchKernelGGL((k_wres1x1<K, CW, bf16_t>), dim3(grid), dim3(512), 0, s, w);
+        auto go = [&](auto h) {
+            using H = decltype(h);
+            if (res) hipLaunchKernelGGL((k_wres1x1<K, CW, true, H>), dim3(grid), dim3(512), 0, s, w);
+            else hipLaunchKernelGGL((k_wres1x1<K, CW, false, H>), dim3(grid), dim3(512), 0, s, w);
+        };
+        if (f16) go(f16_t{});
+        else go(bf16_t{});
     }
 }
 }  // namespace
@@ -897,9 +924,13 @@ bool launch_stream1x1(const ConvArgs& a, hipStream_t s, bool f16) {
     if (a.P < 4096 || (long long)a.n * a.h * a.w_ * a.cin >= (1ll << 31)) return false;
     const bool res = a.flags & RR_CONV_RESIDUAL;
     const int K = a.cin, C = a.cout;
-    if (g_wres && res && a.stride == 1 && a.h == a.ho && a.w_ == a.wo && (a.ldy & 7) == 0) {
-        if (K == 512 && C == 2048) { launch_wres<512, 32>(a, s, f16); return true; }
-        if (K == 256 && C == 1024) { launch_wres<256, 64>(a, s, f16); return true; }
+    if (g_wres && (a.ldy & 7) == 0 && (a.stride == 1 ? a.h == a.ho && a.w_ == a.wo : !res)) {
+        if (K == 512 && C == 2048 && res) { launch_wres<512, 32>(a, s, f16); return true; }
+        if (K == 256 && C == 1024 && res) { launch_wres<256, 64>(a, s, f16); return true; }
+        if (g_wres >= 2) {  // the non-residual K = 256 / 512 1x1s (projections, mod4 block-1 conv1)
+            if (K == 512 && (C == 256 || C == 1024 || C == 2048) && !res) { launch_wres<512, 32>(a, s, f16); return true; }
+            if (K == 256 && (C == 512 || C == 1024) && !res) { launch_wres<256, 64>(a, s, f16); return true; }
+        }
     }
     // mode 2: the residual 512 -> 2048 1x1 (mod5 conv3) on the 8-phase GEMM;
     // mode 3: also the residual 256 -> 1024 1x1 (mod4 conv3)

@@ -338,7 +338,9 @@ int rr_rank_full(const float* db_f32, long long n, const float* q_f32, int nq, i
  *                        c_out = 128 under RR_TUNE_CONV3X3 = 1; 2: also c_in = c_out = 64; 0 off
  *   RR_TUNE_WRES         1: the residual 256 -> 1024 / 512 -> 2048 1x1s (bottleneck conv3 of
  *                        mod4 / mod5) on the weight-stationary k_wres1x1 (weights in VGPRs,
- *                        activation + residual tiles by LDS-DMA); 0: the streaming 1x1 */
+ *                        activation + residual tiles by LDS-DMA); 2: also the non-residual
+ *                        K = 256 / 512 1x1s (projections, strided or not; mod4 block-1 conv1);
+ *                        0: the streaming 1x1 / 8-phase GEMM */
 enum rr_tune_key { RR_TUNE_GEMM_CONFIG = 0, RR_TUNE_GEMM_STAGES = 1, RR_TUNE_GEMM_WIDE = 2,
                    RR_TUNE_GEMM_ASTAT = 3, RR_TUNE_GEMM_XCD_MAP = 4, RR_TUNE_STREAM_1X1 = 5,
                    RR_TUNE_CONV3X3 = 6, RR_TUNE_GRID_CUS = 7, RR_TUNE_GEMM8 = 8,

@@ -134,6 +134,11 @@ WRES_CASES = [
     (1, 512, 64, 67, 2048, 1, 1, 0, True, True),    # 8 slices of 256 channels
     (4, 256, 48, 64, 1024, 1, 1, 0, True, True),    # chip-filling grid: XCD map on
     (2, 512, 48, 64, 2048, 1, 1, 0, True, False),   # identity activation
+    # RR_TUNE_WRES = 2: the non-residual K = 256 / 512 1x1s, strided or not
+    (1, 512, 65, 67, 256, 1, 1, 0, False, True),    # mod4 block-1 conv1: one slice
+    (2, 512, 130, 70, 1024, 1, 2, 0, False, True),  # mod4 projection (stride 2), ragged last tile
+    (2, 256, 83, 101, 512, 1, 2, 0, False, False),  # mod3 projection (stride 2, odd map)
+    (1, 256, 64, 70, 1024, 1, 1, 0, False, True),
 ]
 
 
@@ -145,11 +150,34 @@ def test_wres1x1(cuda, case, prec):
     from cirtorch import _engine as E
     outs = []
     try:
-        for on in (1, 0):
+        for on in (2, 0):
             E.check(E.lib().rr_set_tuning(14, on), "rr_set_tuning")
             outs.append(_check_conv(cuda, case, prec, True))
     finally:
         E.lib().rr_set_tuning(14, 0)
+    assert torch.equal(outs[0], outs[1])
+
+
+C3W64_CASES = [
+    (2, 64, 48, 64, 64, 3, 1, 1, False, True),     # 24 tiles: fewer than the grid's blocks
+    (3, 64, 64, 96, 64, 3, 1, 1, False, False),
+    (16, 64, 48, 128, 64, 3, 1, 1, False, True),   # 384 tiles over 256 blocks
+]
+
+
+@pytest.mark.parametrize("case", C3W64_CASES)
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_c3w64_bit_identical(cuda, case, prec):
+    """mod2 3x3 with the weights in VGPRs (RR_TUNE_CONV3X3 = 9): exact vs float64 and
+    bit-identical to the A-stationary direct kernel (same (tap, half-step) order)."""
+    from cirtorch import _engine as E
+    outs = []
+    try:
+        for mode in (9, 4):
+            E.check(E.lib().rr_set_tuning(6, mode), "rr_set_tuning")
+            outs.append(_check_conv(cuda, case, prec, True))
+    finally:
+        E.lib().rr_set_tuning(6, 1)
     assert torch.equal(outs[0], outs[1])
 
 
@@ -166,7 +194,8 @@ CONV3_CASES = [
 
 @pytest.mark.parametrize("case", CONV3_CASES)
 @pytest.mark.parametrize("mode,prec", [(1, "bf16"), (2, "bf16"), (3, "bf16"), (4, "bf16"), (6, "bf16"), (7, "bf16"),
-                                       (8, "bf16"), (0, "bf16"), (1, "fp16"), (8, "fp16"), (0, "fp16")])
+                                       (8, "bf16"), (9, "bf16"), (0, "bf16"), (1, "fp16"), (8, "fp16"), (9, "fp16"),
+                                       (0, "fp16")])
 def test_conv3x3_direct(cuda, case, mode, prec):
     """Direct 3x3 kernel (modes 1-4, 6: auto / 8x32 / 4x32 tiles / A-stationary wave layouts) and the
     implicit-GEMM fallback (mode 0) against the float64 reference."""
