@@ -600,7 +600,7 @@ void launch_c3(const ConvArgs& a, hipStream_t s, bool f16) {
 
 }  // namespace
 
-int g_c3w64 = 0;       // mod2 3x3 on k_c3w64 under RR_TUNE_CONV3X3 = 1 (9 forces it)
+int g_c3w64 = 1;       // mod2 3x3 on k_c3w64 under RR_TUNE_CONV3X3 = 1 (9 forces it)
 int g_conv3_mode = 1;  // rr_set_tuning(RR_TUNE_CONV3X3): 0 off, 1 auto, 2 / 3 prefer 8x32 / 4x32 tiles,
                        // 4 / 6 A-stationary with 1x8 / 1x4 waves (auto: 2x4), 7 3-stage weight ring,
                        // 8 256-channel x 6x32 tiles (auto where c_out % 256 == 0 and h % 6 == 0)

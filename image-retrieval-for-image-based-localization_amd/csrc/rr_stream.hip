@@ -863,7 +863,7 @@ void launch_s_t(const ConvArgs& a, hipStream_t s) {
 }  // namespace
 
 int g_stream_mode = 1;  // rr_set_tuning(RR_TUNE_STREAM_1X1): 0 off, 1 auto, 2 / 3 see launch_stream1x1
-int g_wres = 0;         // rr_set_tuning(RR_TUNE_WRES)
+int g_wres = 2;         // rr_set_tuning(RR_TUNE_WRES)
 
 namespace {
 template <int K, int CW>

@@ -314,7 +314,9 @@ int rr_rank_full(const float* db_f32, long long n, const float* q_f32, int nq, i
  *                        halo patches for the bf16 stride-1 3x3 convs;
  *                        2 / 3 prefer its 8x32 / 4x32 pixel tiles, 4 / 6 use
  *                        1x8 / 1x4 waves for the c_in = 64 A-stationary form,
- *                        7 a 3-stage weight ring, 8 256-channel x 6x32 tiles
+ *                        7 a 3-stage weight ring, 8 256-channel x 6x32 tiles,
+ *                        9 the c_in = c_out = 64 form with the weights in VGPRs
+ *                        (k_c3w64; also what 1 picks for that shape)
  *   RR_TUNE_GRID_CUS     cap on the CUs one persistent launch spreads over
  *                        (0 = all; e.g. half the chip for two concurrent streams)
  *   RR_TUNE_GEMM8        0 off, 1 auto, 2 forced: the 8-phase staggered 256x256 GEMM for eligible
@@ -339,8 +341,8 @@ int rr_rank_full(const float* db_f32, long long n, const float* q_f32, int nq, i
  *   RR_TUNE_WRES         1: the residual 256 -> 1024 / 512 -> 2048 1x1s (bottleneck conv3 of
  *                        mod4 / mod5) on the weight-stationary k_wres1x1 (weights in VGPRs,
  *                        activation + residual tiles by LDS-DMA); 2: also the non-residual
- *                        K = 256 / 512 1x1s (projections, strided or not; mod4 block-1 conv1);
- *                        0: the streaming 1x1 / 8-phase GEMM */
+ *                        K = 256 / 512 1x1s (projections, strided or not; mod4 block-1 conv1;
+ *                        default); 0: the streaming 1x1 / 8-phase GEMM */
 enum rr_tune_key { RR_TUNE_GEMM_CONFIG = 0, RR_TUNE_GEMM_STAGES = 1, RR_TUNE_GEMM_WIDE = 2,
                    RR_TUNE_GEMM_ASTAT = 3, RR_TUNE_GEMM_XCD_MAP = 4, RR_TUNE_STREAM_1X1 = 5,
                    RR_TUNE_CONV3X3 = 6, RR_TUNE_GRID_CUS = 7, RR_TUNE_GEMM8 = 8,

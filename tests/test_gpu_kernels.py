@@ -99,10 +99,12 @@ def test_conv_stream1x1(cuda, case, mode, prec):
     (mode 0) on the same shapes."""
     from cirtorch import _engine as E
     E.check(E.lib().rr_set_tuning(5, mode), "rr_set_tuning")
+    E.check(E.lib().rr_set_tuning(14, 0), "rr_set_tuning")  # the streaming kernel, not k_wres1x1
     try:
         _check_conv(cuda, case, prec, True)
     finally:
         E.lib().rr_set_tuning(5, 1)
+        E.lib().rr_set_tuning(14, 2)
 
 
 XCD_CASES = [
@@ -119,12 +121,14 @@ def test_stream1x1_xcd_map(cuda, case):
     pure block-to-work remapping: exact vs float64, bit-identical to the plain order."""
     from cirtorch import _engine as E
     outs = []
+    E.check(E.lib().rr_set_tuning(14, 0), "rr_set_tuning")  # the streaming kernel, not k_wres1x1
     try:
         for xcd in (1, 0):
             E.check(E.lib().rr_set_tuning(12, xcd), "rr_set_tuning")
             outs.append(_check_conv(cuda, case, "bf16", True))
     finally:
         E.lib().rr_set_tuning(12, 1)
+        E.lib().rr_set_tuning(14, 2)
     assert torch.equal(outs[0], outs[1])
 
 
@@ -154,7 +158,7 @@ def test_wres1x1(cuda, case, prec):
             E.check(E.lib().rr_set_tuning(14, on), "rr_set_tuning")
             outs.append(_check_conv(cuda, case, prec, True))
     finally:
-        E.lib().rr_set_tuning(14, 0)
+        E.lib().rr_set_tuning(14, 2)
     assert torch.equal(outs[0], outs[1])
 
 

@@ -1,6 +1,7 @@
 #!/bin/bash
-# Round-3 GPU step runner: bash tools/r03_step.sh <tag> <step...>
-#   steps: ktest:<pytest -k expr>  layers:<tune>  bench  benchq  tests  prof
+# GPU step runner: bash tools/gpu_steps.sh <tag> <step...>
+#   steps: ktest:<pytest -k expr>  pytest:<files>  layers:<tune>  bench  benchq:<tune>  tests  prof  pmc
+#          knnprof:<Q>:<screen>  stem
 # Each GPU step has its own time limit; the first failure ends the script.
 set -e
 TAG=$1; shift
@@ -24,7 +25,7 @@ for STEP in "$@"; do
       tail -2 "$OUT/pytest_$i.log" ;;
     layers:*)
       TUNE=${STEP#layers:}
-      timeout -k 10 300 python -u tools/layer_bench.py --batch 128 --tune "$TUNE" > "$OUT/layers_$i.txt" 2>&1 || { tail -20 "$OUT/layers_$i.txt"; exit 1; }
+      timeout -k 10 300 python -u tools/layer_bench.py --batch 128 --precision fp16 --tune "$TUNE" > "$OUT/layers_$i.txt" 2>&1 || { tail -20 "$OUT/layers_$i.txt"; exit 1; }
       echo "== layers tune=$TUNE"; grep -v amdgpu.ids "$OUT/layers_$i.txt" ;;
     bench)
       timeout -k 10 600 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -20 "$OUT/bench.err"; exit 1; }
@@ -56,6 +57,15 @@ d=json.loads(open('$OUT/benchenv_$i.json').read().strip().splitlines()[-1]); pri
         --output-format csv -- python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --no-extras --latency 0 --pcie-steps 0 --fp16-steps 0 \
         > "$OUT/prof_bench.json" 2> "$OUT/prof.err") || { tail -20 "$OUT/prof.err"; exit 1; }
       tail -c 1500 "$OUT/prof_bench.json" ;;
+    knnprof:*)
+      QS=${STEP#knnprof:}; Q=${QS%%:*}; SCR=${QS#*:}
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/knnprof_${Q}_$SCR" -o run \
+        --output-format csv -- python3 "$ROOT/tools/knn_probe.py" --q $Q --screen $SCR > "$OUT/knnprof_${Q}_$SCR.txt" 2>&1) \
+        || { tail -20 "$OUT/knnprof_${Q}_$SCR.txt"; exit 1; }
+      grep search "$OUT/knnprof_${Q}_$SCR.txt" ;;
+    stem)
+      timeout -k 10 200 python -u tools/stem_ab.py > "$OUT/stem_ab.json" 2>&1 || { tail -20 "$OUT/stem_ab.json"; exit 1; }
+      tail -c 600 "$OUT/stem_ab.json" ;;
     pmc)
       timeout -k 10 900 bash "$ROOT/tools/pmc_round.sh" "gpurun_out/$TAG/pmc" > "$OUT/pmc.log" 2>&1 || { tail -20 "$OUT/pmc.log"; exit 1; }
       tail -2 "$OUT/pmc.log" ;;

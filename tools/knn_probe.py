@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--n", type=int, default=1_000_000)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--tune", default="", help="rr_set_tuning pairs key=value[,key=value]")
+    ap.add_argument("--screen", default="int8", help="screening dtype (int8 / fp16 / bf16 / fp32)")
     args = ap.parse_args()
     from cirtorch import _ops
     from cirtorch import _engine as E
@@ -25,7 +26,7 @@ def main():
     from cirtorch.search import KnnIndex
     db = _ops.fill_unit_rows(args.n, 2048, seed=0xDB5EED)
     q = _ops.fill_unit_rows(args.q, 2048, seed=0x0E5EED)
-    idx = KnnIndex(db, "bf16")
+    idx = KnnIndex(db, args.screen)
     idx.search(q, 100)
     torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -34,7 +35,8 @@ def main():
         idx.search(q, 100)
     b.record()
     torch.cuda.synchronize()
-    print("search Q=%d N=%d tune=%s: %.3f ms" % (args.q, args.n, args.tune, a.elapsed_time(b) / args.reps))
+    print("search Q=%d N=%d screen=%s tune=%s: %.3f ms" % (args.q, args.n, args.screen, args.tune,
+                                                          a.elapsed_time(b) / args.reps))
 
 
 if __name__ == "__main__":
