@@ -91,6 +91,8 @@ def parse():
                     help="rehearsal on a 1-GPU box: every rank on cuda:0 (with --dist-backend gloo)")
     ap.add_argument("--extract-priority", type=int, default=int(os.environ.get("RR_BENCH_PRIO", "0")),
                     help="1: run the extraction on a high-priority stream (the overlapped search keeps the default)")
+    ap.add_argument("--match-priority", type=int, default=int(os.environ.get("RR_BENCH_MPRIO", "0")),
+                    help="1: run the overlapped search on a high-priority stream (its blocks go first when a CU frees)")
     ap.add_argument("--tune", default="", help="developer A/B: rr_set_tuning pairs key=value[,key=value]")
     ap.add_argument("--alt-steps", "--fp16-steps", dest="alt_steps", type=int, default=10,
                     help="steps of the end-to-end line in the other 16-bit precision (e2e_bf16 beside an fp16 "
@@ -671,7 +673,8 @@ def main():
         # priority) fills the extractor's gaps instead of competing with it
         torch.cuda.set_stream(torch.cuda.Stream(dev, priority=-1))
     main_stream = torch.cuda.current_stream(dev)
-    match_stream = torch.cuda.Stream(dev) if args.overlap else main_stream
+    match_stream = (torch.cuda.Stream(dev, priority=-1 if args.match_priority else 0) if args.overlap
+                    else main_stream)
 
     state = {"net": net, "index": index}
 

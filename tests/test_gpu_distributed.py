@@ -54,7 +54,8 @@ def _worker(rank, world, port, n, d, q, k, prec, ret):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n,prec", [(2, 30000, "bf16"), (2, 20011, "fp16"), (3, 2, "fp32")])
+@pytest.mark.parametrize("world,n,prec", [(2, 30000, "bf16"), (2, 20011, "fp16"), (3, 2, "fp32"), (2, 70001, "int8"),
+                                          (3, 5, "int8")])
 def test_sharded_real_kernels_equal_single_search(cuda, world, n, prec):
     from cirtorch import _ops
     from cirtorch.search import KnnIndex

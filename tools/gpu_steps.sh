@@ -63,6 +63,11 @@ d=json.loads(open('$OUT/benchenv_$i.json').read().strip().splitlines()[-1]); pri
         --output-format csv -- python3 "$ROOT/tools/knn_probe.py" --q $Q --screen $SCR > "$OUT/knnprof_${Q}_$SCR.txt" 2>&1) \
         || { tail -20 "$OUT/knnprof_${Q}_$SCR.txt"; exit 1; }
       grep search "$OUT/knnprof_${Q}_$SCR.txt" ;;
+    knnenv:*)
+      QE=${STEP#knnenv:}; Q=${QE%%:*}; ENVV=${QE#*:}
+      env $ENVV timeout -k 10 300 python -u tools/knn_probe.py --q $Q --screen int8 --reps 20 > "$OUT/knnenv_$i.txt" 2>&1 \
+        || { tail -20 "$OUT/knnenv_$i.txt"; exit 1; }
+      echo "env=$ENVV $(grep search "$OUT/knnenv_$i.txt")" ;;
     stem)
       timeout -k 10 200 python -u tools/stem_ab.py > "$OUT/stem_ab.json" 2>&1 || { tail -20 "$OUT/stem_ab.json"; exit 1; }
       tail -c 600 "$OUT/stem_ab.json" ;;
