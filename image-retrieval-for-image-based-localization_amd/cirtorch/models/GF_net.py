@@ -301,8 +301,10 @@ def _pinned_chain(slot, shape, dtype):
 
 
 def _default_workers():
-    """decode threads: the CPUs this process may run on, at most 16"""
+    """decode threads: the CPUs this process may run on, at most 16 (RR_EV_WORKERS overrides)"""
     import os
+    if os.environ.get("RR_EV_WORKERS"):
+        return max(1, int(os.environ["RR_EV_WORKERS"]))
     try:
         n = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
