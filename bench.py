@@ -93,6 +93,9 @@ def parse():
                     help="1: run the extraction on a high-priority stream (the overlapped search keeps the default)")
     ap.add_argument("--match-priority", type=int, default=int(os.environ.get("RR_BENCH_MPRIO", "0")),
                     help="1: run the overlapped search on a high-priority stream (its blocks go first when a CU frees)")
+    ap.add_argument("--graph", type=int, default=int(os.environ.get("RR_BENCH_GRAPH", "1")),
+                    help="1: each extractor chain is recorded once as a hipGraph (torch.cuda.CUDAGraph) reading the "
+                         "resident images in place and replayed every step (all kernels still run); 0: eager launches")
     ap.add_argument("--tune", default="", help="developer A/B: rr_set_tuning pairs key=value[,key=value]")
     ap.add_argument("--alt-steps", "--fp16-steps", dest="alt_steps", type=int, default=10,
                     help="steps of the end-to-end line in the other 16-bit precision (e2e_bf16 beside an fp16 "
@@ -694,6 +697,26 @@ def main():
 
     EB = max(1, min(args.extract_batch, B))
 
+    graphs = {}  # (id(net), chain) -> (hipGraph, its static output)
+
+    def run_chain(c):
+        """one extractor chain; --graph: replay of its recorded launches (the first call runs
+        eagerly once -- weight packing, workspaces -- then records)"""
+        x = images[c:c + EB]
+        if not args.graph:
+            return state["net"].extract(x)
+        key = (id(state["net"]), c)
+        if key not in graphs:
+            state["net"].extract(x)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                out = state["net"].extract(x)
+            graphs[key] = (g, out)
+        g, out = graphs[key]
+        g.replay()
+        return out.clone()  # the static output is overwritten by the next replay
+
     def extract_all(record):
         """the step's B images as B/EB extractor chains -> D x B descriptors"""
         descs = []
@@ -701,7 +724,7 @@ def main():
             if record:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(main_stream)
-            descs.append(state["net"].extract(images[c:c + EB]))
+            descs.append(run_chain(c))
             if record:
                 e1.record(main_stream)
                 ev_pairs.append((e0, e1))
@@ -759,6 +782,8 @@ def main():
                 dist.barrier()
             el_a = max_over_ranks(time.perf_counter() - ta)
             state["net"], state["index"] = saved
+            for key in [k_ for k_ in graphs if k_[0] == id(net_a)]:
+                del graphs[key]
             e2e_alt = {"value": world * B * args.alt_steps / el_a, "unit": "images/s", "dtype": alt,
                        "ms_per_step": el_a / args.alt_steps * 1e3, "steps": args.alt_steps,
                        "note": "the headline step (extract B images + top-k search of all queries vs the sharded "
@@ -1034,7 +1059,8 @@ def main():
                                   if args.overlap else ""),
                    "global_batch": B * world, "extract_batch": EB, "image": [3, H, W], "db_rows": args.db_rows,
                    "dim": args.dim,
-                   "k": args.k, "parallelism": "dp%d (images) x db-shard%d" % (world, world)},
+                   "k": args.k, "parallelism": "dp%d (images) x db-shard%d" % (world, world),
+                   "launch": "extractor chains replayed as hipGraphs" if args.graph else "eager launches"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                      "frac": achieved / peak, "traffic": traffic, "traffic_note": traffic_note,
                      "algorithmic_bytes": bytes_img * B,
