@@ -441,22 +441,35 @@ __global__ void __launch_bounds__(64 * WC * WP) k_conv3x3(ConvArgs a, int tiles_
 // ---------------------------------------------------------------------------
 // mod2 3x3 (c_in = c_out = 64) with the weights in VGPRs.  k_conv3x3's
 // A-stationary form reads both operands from LDS: per MFMA 0.75 KiB (2 A + 4 B
-// fragments per 8 MFMAs), 1.5x what the LDS port delivers at the MFMA rate, and
-// the 72 KiB weight image leaves room for only two halo patches.  Here each
-// wave keeps its 32 output channels x all 576 K of the PERM32 weights in VGPRs
-// (2 x 18 fragments, 144 VGPRs) for the whole launch, so a B fragment read from
-// LDS feeds 2 MFMAs and nothing else is read; the LDS holds three 8x32-tile
-// halo patches (48 KiB each), prefetched two tiles ahead by LDS-DMA.
+// fragments per 8 MFMAs), and the 72 KiB weight image leaves room for only two
+// halo patches.  Here each wave keeps its 32 output channels x all 576 K of
+// the PERM32 weights in VGPRs (2 x 18 fragments, 144 VGPRs) for the whole
+// launch, so a B fragment read from LDS feeds 2 MFMAs and nothing else is
+// read; the LDS holds three 8x32-tile halo patches, prefetched two tiles ahead
+// by LDS-DMA.  The patch rows are laid out 40 pixel slots apart (34 used): a
+// multiple of 8, so the chunk swizzle (chunk ^ (slot & 7)) is the same on
+// every patch row and the 18 K-steps' fragment addresses are 24 per-lane
+// bases (pixel fragment x tap column x half-step) plus immediate row offsets
+// — no address arithmetic between the MFMAs.
 // Persistent block per CU, 8 waves = 2 channel halves x 4 pixel quarters;
 // tiles walked XCD-contiguously (the 32 tiles an XCD holds at once are 4 tile
 // rows of one image: vertical halo re-reads hit its L2).  Accumulation order
 // (tap, half-step) equals k_conv3x3's: bit-identical outputs.
+// A value loaded once before a loop (weights kept in VGPRs): passing it through an
+// empty asm makes the asm its producer, so the compiler's wait for the load sits
+// before the loop instead of (counted against the loop's own LDS-DMA / stores,
+// which it cannot see) in front of every use inside it.
+__device__ __forceinline__ void pin_loaded(uint4& v) {
+    asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+}
+
 template <typename HT>
 __global__ void __launch_bounds__(512, 1) k_c3w64(ConvArgs a, int tiles_w, int tiles_hw, int ntiles) {
-    constexpr int TH = 8, TW = 32, TP = TH * TW, PC = TW + 2, NPIX = (TH + 2) * PC;  // 340 patch pixels
-    constexpr int NDW = 6, PBYTES = 8 * NDW * 1024;  // patch: 48 wave-instructions of 8 pixels x 128 B
+    constexpr int TH = 8, TW = 32, TP = TH * TW, PCW = TW + 2, PITCH = 40;  // 34 patch columns, 40 slots
+    constexpr int NSLOT = (TH + 2) * PITCH, NP = NSLOT / 8;                 // 400 slots, 50 pieces of 8
+    constexpr int PBYTES = NP * 1024;
     constexpr int NBUF = 3, FN = TP / 4 / 16, NST = FN;  // per wave: 4 pixel fragments, 4 epilogue stores
-    static_assert(8 * NDW * 8 >= NPIX, "patch pieces");
+    static_assert(PITCH % 8 == 0 && NSLOT % 8 == 0, "row-invariant swizzle");
     __shared__ __attribute__((aligned(1024))) char smem[NBUF * PBYTES];
     __shared__ __attribute__((aligned(16))) float sS[64], sH[64];
 
@@ -477,6 +490,10 @@ __global__ void __launch_bounds__(512, 1) k_c3w64(ConvArgs a, int tiles_w, int t
         for (int s = 0; s < 18; ++s)
             areg[i][s] = *reinterpret_cast<const uint4*>((const bf16_t*)a.w + (long long)(32 * wc + 16 * i + r16) * 576 +
                                                          (s >> 1) * 64 + 32 * (s & 1) + 8 * kq);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int s = 0; s < 18; ++s) pin_loaded(areg[i][s]);
     __syncthreads();
 
     // XCD-contiguous walk: round i, XCD x = b & 7 takes tiles [i G + x G/8, ... + G/8)
@@ -484,25 +501,34 @@ __global__ void __launch_bounds__(512, 1) k_c3w64(ConvArgs a, int tiles_w, int t
     auto tile_id = [&](int i) { return i * G + (b & 7) * (G >> 3) + (b >> 3); };
     const pi32x4_t rsX = prsrc(a.x, (unsigned)((long long)a.n * H * W * 64 * 2));
     const unsigned lds0 = (unsigned)(unsigned long long)smem;
+    // pieces d = wave + 8 u (50 per patch: waves 0-1 issue 7, the others 6)
+    const int nd = (NP - wave + 7) / 8;
     auto patch_dma = [&](int t, int buf) {
         const int img = t / tiles_hw, rem = t - img * tiles_hw, th = rem / tiles_w;
         const int oh0 = th * TH, ow0 = (rem - th * tiles_w) * TW;
 #pragma unroll
-        for (int u = 0; u < NDW; ++u) {
-            const int d = NDW * wave + u, q = d * 8 + lrow;
-            const int pr = q / PC, pc = q - pr * PC;
+        for (int u = 0; u < 7; ++u) {
+            const int d = wave + 8 * u, q = d * 8 + lrow;
+            if (d >= NP) break;  // wave-uniform
+            const int pr = q / PITCH, pc = q - pr * PITCH;
             const int hh = oh0 - 1 + pr, ww = ow0 - 1 + pc;
             unsigned off = POOB;
-            if (t < ntiles && q < NPIX && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W)
+            if (t < ntiles && pc < PCW && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W)
                 off = (unsigned)(((((long long)img * H + hh) * W + ww) * 64 + ((lch ^ lrow) << 3)) * 2);
             pdma16(rsX, off, lds0 + buf * PBYTES + d * 1024);
         }
     };
-    int bq[FN];
+    // per-lane fragment address bases: pixel fragment j, tap column dx, half-step hs
+    int rel[FN][3][2];
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
         const int p = wp * (TP / 4) + j * 16;
-        bq[j] = (p / TW) * PC + (p % TW) + r16;
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+            const int q = (p / TW) * PITCH + (p % TW) + r16 + dx;
+#pragma unroll
+            for (int hs = 0; hs < 2; ++hs) rel[j][dx][hs] = q * 128 + (((kq + 4 * hs) ^ (q & 7)) << 4);
+        }
     }
     bf16_t* __restrict__ Y = (bf16_t*)a.y;
     const bool leaky = a.act == RR_ACT_LEAKY;
@@ -510,22 +536,32 @@ __global__ void __launch_bounds__(512, 1) k_c3w64(ConvArgs a, int tiles_w, int t
     const int nmine = (ntiles - 1 - (b >> 3) - (b & 7) * (G >> 3)) >= 0
                           ? (ntiles - 1 - (b & 7) * (G >> 3) - (b >> 3)) / G + 1 : 0;
     if (nmine == 0) return;
-    // every wave issues exactly NDW pieces per patch (pieces past the patch write
-    // zeros into the buffer's tail), so the counted waits below are uniform
+    // a wave issues the same nd pieces for every patch (past the last tile: zeros),
+    // so its counted waits are fixed: nd for the next patch (+ NST stores)
     patch_dma(tile_id(0), 0);
     patch_dma(tile_id(1), 1);
     for (int i = 0; i < nmine; ++i) {
         // patch(i) landed: younger are patch(i + 1) and tile i - 1's stores
-        if (i == 0) pwait_barrier<NDW>();
-        else pwait_barrier<NDW + NST>();
+        if (nd == 7) {
+            if (i == 0) pwait_barrier<7>();
+            else pwait_barrier<7 + NST>();
+        } else {
+            if (i == 0) pwait_barrier<6>();
+            else pwait_barrier<6 + NST>();
+        }
         patch_dma(tile_id(i + 2), (i + 2) % NBUF);
         const char* Ps = smem + (i % NBUF) * PBYTES;
-        int bql[FN];
+        const char* base[FN][3][2];
 #pragma unroll
-        for (int j = 0; j < FN; ++j) {
-            bql[j] = bq[j];
-            asm volatile("" : "+v"(bql[j]));
-        }
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+                for (int hs = 0; hs < 2; ++hs) {
+                    int r = rel[j][dx][hs];
+                    asm volatile("" : "+v"(r));  // per-tile opaque copy: bases stay 24 VGPRs
+                    base[j][dx][hs] = Ps + r;
+                }
         pf32x4_t acc[2][FN];
 #pragma unroll
         for (int ii = 0; ii < 2; ++ii)
@@ -533,13 +569,10 @@ __global__ void __launch_bounds__(512, 1) k_c3w64(ConvArgs a, int tiles_w, int t
             for (int j = 0; j < FN; ++j) acc[ii][j] = (pf32x4_t){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < 18; ++s) {
-            const int tap = s >> 1, ch = kq + 4 * (s & 1), toff = (tap / 3) * PC + tap % 3;
+            const int tap = s >> 1, hs = s & 1, dy = tap / 3, dx = tap % 3;
             uint4 fb[FN];
 #pragma unroll
-            for (int j = 0; j < FN; ++j) {
-                const int q = bql[j] + toff;
-                fb[j] = *reinterpret_cast<const uint4*>(Ps + q * 128 + ((ch ^ (q & 7)) << 4));
-            }
+            for (int j = 0; j < FN; ++j) fb[j] = *reinterpret_cast<const uint4*>(base[j][dx][hs] + dy * PITCH * 128);
 #pragma unroll
             for (int ii = 0; ii < 2; ++ii)
 #pragma unroll

@@ -441,6 +441,14 @@ __global__ void __launch_bounds__(512) k_stream_pair(PairArgs a) {
 // y and z are bit-identical to them.
 typedef __attribute__((ext_vector_type(4))) int si32x4_t;
 
+// A value loaded once before a loop (weights kept in VGPRs): passing it through an
+// empty asm makes the asm its producer, so the compiler's wait for the load sits
+// before the loop instead of (counted against the loop's own LDS-DMA / stores,
+// which it cannot see) in front of every use inside it.
+__device__ __forceinline__ void pin_loaded(uint4& v) {
+    asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+}
+
 __device__ __forceinline__ void sdma16(si32x4_t rsrc, unsigned voff, unsigned lds_addr) {
     unsigned keep;
     lds_addr = __builtin_amdgcn_readfirstlane(lds_addr);
@@ -506,6 +514,12 @@ __global__ void __launch_bounds__(512, 1) k_pair_mid(PairMidArgs a) {
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk)
         a1[kk] = *reinterpret_cast<const uint4*>(a.w1 + (long long)(16 * wave + r16) * C3 + 32 * kk + 8 * kq);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) pin_loaded(a3[i][kk]);
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) pin_loaded(a1[kk]);
     __syncthreads();
 
     const long long P = a.P;
@@ -719,6 +733,10 @@ __global__ void __launch_bounds__(512, 1) k_wres1x1(WresArgs a) {
 #pragma unroll
         for (int kk = 0; kk < NK; ++kk)
             areg[i][kk] = *reinterpret_cast<const uint4*>(a.w + (long long)(cw0 + 16 * i + r16) * K + 32 * kk + 8 * kq);
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int kk = 0; kk < NK; ++kk) pin_loaded(areg[i][kk]);
     __syncthreads();
 
     const long long P = a.P;
