@@ -624,7 +624,7 @@ static void launch_cfg3(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
 // (two 64-deep MFMAs), the accumulators are exact int32 and the epilogue converts
 // them to float (K1, natural row order, float out only).
 template <typename T, typename TO, int KM, bool PERM>
-__global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int ntiles) {
+__global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int ntiles, int pmajor) {
     constexpr bool I8 = std::is_same<T, int8_t>::value;
     static_assert(sizeof(T) == 2 || (I8 && KM == 1 && !PERM && sizeof(TO) == 4), "16-bit operands / int8 scores");
     constexpr bool K1 = KM == 1, tapu = KM == 2;
@@ -682,9 +682,14 @@ __global__ void __launch_bounds__(512, 1) k_gemm8(ConvArgs a, int tiles_p, int n
     i32x4_t rsA;
     unsigned a_off[2][2], b_base[2][2];
     int b_hi[2][2], b_wi[2][2];
+    // tile order: channel-major (the pixel tiles of one channel tile consecutive: the kNN
+    // score GEMM's query tiles of one database tile share its rows in one XCD's L2) or
+    // pixel-major (pmajor: the channel tiles of one pixel tile consecutive, so a conv's
+    // input tile is fetched into one XCD's L2 once for all its channel tiles)
+    const int tiles_c = ntiles / tiles_p;
     auto setup = [&](int t) {
-        c0 = (t / tiles_p) * 256;
-        p0 = (t % tiles_p) * 256;
+        c0 = (pmajor ? t % tiles_c : t / tiles_p) * 256;
+        p0 = (pmajor ? t / tiles_c : t % tiles_p) * 256;
         const long long arows = min(256, a.cout - c0);
         rsA = make_rsrc((const char*)a.w + (long long)c0 * a.kp * ESZ, (unsigned)(arows * a.kp * ESZ));
 #pragma unroll
@@ -1620,6 +1625,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm8a(ConvArgs a, int tiles_p, int 
 
 static int g_gemm8 = -1;  // rr_set_tuning(RR_TUNE_GEMM8) / RR_GEMM8: 0 off, 1 auto (default), 2 force where legal
 static bool g_gemm8_tile = false;  // RR_TUNE_GEMM8 value | 4: one block per tile instead of persistent blocks
+static bool g_gemm8_pmajor = true;  // RR_TUNE_GEMM8 value | 64: conv tiles channel-major
 
 // 16-bit operands, 1x1 or tap-uniform im2col, an even number of 64-deep
 // K-steps, 31-bit operand offsets, and (auto) enough 256 x 256 tiles to fill
@@ -1670,7 +1676,9 @@ static bool try_gemm8(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
                                                (std::is_same<T, TO>::value && short_k1));
         // (a grid below 8 blocks would leave some XCD's tile range without a block)
         const dim3 g((unsigned)(!persist || cus < 8 || ntiles < cus ? ntiles : cus)), b(512);
-#define RR_G8(KMV, PV) hipLaunchKernelGGL((k_gemm8<T, TO, KMV, PV>), g, b, 0, s, a, tiles_p, (int)ntiles)
+        // conv GEMMs (16-bit out) walk their tiles pixel-major (RR_TUNE_GEMM8 | 64: channel-major)
+        const int pmajor = std::is_same<T, TO>::value && g_gemm8_pmajor && tiles_c > 1;
+#define RR_G8(KMV, PV) hipLaunchKernelGGL((k_gemm8<T, TO, KMV, PV>), g, b, 0, s, a, tiles_p, (int)ntiles, pmajor)
         if constexpr (std::is_same<T, TO>::value) {
             if (perm) {
                 if (km == 1) RR_G8(1, true);
@@ -1768,7 +1776,7 @@ int gemm_scores_i8(const ConvArgs& a, hipStream_t s) {
     const long long ntiles = (long long)tiles_p * ((a.cout + 255) / 256);
     if (ntiles >= (1ll << 31)) return fail(RR_EINVAL, "int8 score GEMM: too many tiles");
     const dim3 g((unsigned)(cus < 8 || ntiles < cus ? ntiles : cus));
-    hipLaunchKernelGGL((k_gemm8<int8_t, float, 1, false>), g, dim3(512), 0, s, a, tiles_p, (int)ntiles);
+    hipLaunchKernelGGL((k_gemm8<int8_t, float, 1, false>), g, dim3(512), 0, s, a, tiles_p, (int)ntiles, 0);
     return RR_OK;
 }
 
@@ -1840,6 +1848,7 @@ void set_gemm_tuning(int key, int value) {
         g_gemm8a = !(value >= 0 && (value & 16));
         g_gemm8s = !(value >= 0 && (value & 32));
         g_gemm8_tile = value >= 0 && (value & 4);
+        g_gemm8_pmajor = !(value >= 0 && (value & 64));
         value = value < 0 ? 0 : value & 3;
         g_gemm8 = value > 2 ? 2 : value;
     }
