@@ -709,9 +709,15 @@ def main():
         if key not in graphs:
             state["net"].extract(x)
             torch.cuda.synchronize()
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                out = state["net"].extract(x)
+            try:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    out = state["net"].extract(x)
+            except RuntimeError as e:  # capture refused: run eager from here on, and say so
+                print("bench: hipGraph capture failed (%s); extracting with eager launches" % e, file=sys.stderr)
+                args.graph = 0
+                torch.cuda.synchronize()
+                return state["net"].extract(x)
             graphs[key] = (g, out)
         g, out = graphs[key]
         g.replay()
