@@ -1220,15 +1220,8 @@ __global__ void __launch_bounds__(512, 1) k_gemm8h(ConvArgs a, int ntiles) {
 // stage is complete once at most 6 (R - 1) + 4 younger operations remain.
 // T = int8_t: int8-quantised rows on v_mfma_i32_16x16x64_i8 (see k_gemm8): the same
 // 128-B K-steps carry 128 elements, accumulators are exact int32, scores float(acc).
-typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_nt_t;
-// a once-read database row fragment, loaded nontemporal (not kept in L2 / MALL for re-use)
-__device__ __forceinline__ uint4 ld16_nt(const void* p) {
-    const u32x4_nt_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_nt_t*>(p));
-    return make_uint4(v.x, v.y, v.z, v.w);
-}
-
 template <typename T, int R>
-__global__ void __launch_bounds__(512, 1) k_gemm8s(ConvArgs a, int ntiles, int db_nt) {
+__global__ void __launch_bounds__(512, 1) k_gemm8s(ConvArgs a, int ntiles) {
     constexpr bool I8 = std::is_same<T, int8_t>::value;
     static_assert((sizeof(T) == 2 || I8) && 6 * (R - 1) + 4 <= 63, "16-bit / int8 operands, vmcnt range");
     constexpr int ESZ = sizeof(T), VEC = 16 / ESZ, HT = 16384, NB = R + 1;
@@ -1292,8 +1285,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm8s(ConvArgs a, int ntiles, int d
         for (int g = 0; g < 2; ++g)
 #pragma unroll
             for (int hs = 0; hs < 2; ++hs)
-                dst[g][hs] = db_nt ? ld16_nt(arow[g] + ki * 128 + hs * 64)
-                                   : *reinterpret_cast<const uint4*>(arow[g] + ki * 128 + hs * 64);
+                dst[g][hs] = *reinterpret_cast<const uint4*>(arow[g] + ki * 128 + hs * 64);
         bst = bst + 1 == NB ? 0 : bst + 1;
         if (++ki == nk) {
             ki = 0;
@@ -1703,8 +1695,6 @@ static bool try_gemm8(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
 
 static int g_gemm8h = 1;  // rr_set_tuning(RR_TUNE_GEMM8, value | 8): k_gemm8h off
 static int g_gemm8s = 1;  // rr_set_tuning(RR_TUNE_GEMM8, value | 32): k_gemm8h instead of k_gemm8s
-// RR_GEMM8S_NT=1: the streamed database fragments are loaded nontemporal (A/B knob)
-static const int g_gemm8s_nt = getenv("RR_GEMM8S_NT") ? atoi(getenv("RR_GEMM8S_NT")) : 0;
 
 // k_gemm8h: 16-bit 1x1 score GEMM (float out, natural row order, no affine /
 // residual / activation) with <= 128 "pixels" (queries), long channel dim.
@@ -1728,11 +1718,11 @@ static bool try_gemm8h(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
             // 1.28 at 8, profiles/r03_ab/r03ac_gemm8s_depth_ab.txt); RR_GEMM8S_R = 3 or 6: A/B
             static const int rdepth = getenv("RR_GEMM8S_R") ? atoi(getenv("RR_GEMM8S_R")) : 4;
             if (rdepth == 6)
-                hipLaunchKernelGGL((k_gemm8s<T, 6>), dim3(g), dim3(512), 0, s, a, (int)ntiles, g_gemm8s_nt);
+                hipLaunchKernelGGL((k_gemm8s<T, 6>), dim3(g), dim3(512), 0, s, a, (int)ntiles);
             else if (rdepth == 3)
-                hipLaunchKernelGGL((k_gemm8s<T, 3>), dim3(g), dim3(512), 0, s, a, (int)ntiles, g_gemm8s_nt);
+                hipLaunchKernelGGL((k_gemm8s<T, 3>), dim3(g), dim3(512), 0, s, a, (int)ntiles);
             else
-                hipLaunchKernelGGL((k_gemm8s<T, 4>), dim3(g), dim3(512), 0, s, a, (int)ntiles, g_gemm8s_nt);
+                hipLaunchKernelGGL((k_gemm8s<T, 4>), dim3(g), dim3(512), 0, s, a, (int)ntiles);
         } else {
             hipLaunchKernelGGL((k_gemm8h<T>), dim3((unsigned)ntiles), dim3(512), 0, s, a, (int)ntiles);
         }
@@ -1778,7 +1768,7 @@ int gemm_scores_i8(const ConvArgs& a, hipStream_t s) {
     if (a.P <= 128) {
         const long long ntiles = ((long long)a.cout + 255) / 256;
         const unsigned g = (unsigned)(cus < 8 || ntiles < cus ? ntiles : cus);
-        hipLaunchKernelGGL((k_gemm8s<int8_t, 4>), dim3(g), dim3(512), 0, s, a, (int)ntiles, g_gemm8s_nt);
+        hipLaunchKernelGGL((k_gemm8s<int8_t, 4>), dim3(g), dim3(512), 0, s, a, (int)ntiles);
         return RR_OK;
     }
     if ((a.kp / 128) & 1) return fail(RR_EINVAL, "int8 score GEMM above 128 queries: d must be a multiple of 256");
