@@ -549,11 +549,7 @@ __global__ void __launch_bounds__(512, 1) k_c3w64(ConvArgs a, int tiles_w, int t
             if (i == 0) pwait_barrier<6>();
             else pwait_barrier<6 + NST>();
         }
-        // waves 0-3 issue the next-but-one patch now, waves 4-7 (each SIMD's second wave)
-        // after half of the K-steps: the two waves of a SIMD do not stop their MFMA
-        // streams for the DMA issue at the same time
-        const bool late = wave & 4;
-        if (!late) patch_dma(tile_id(i + 2), (i + 2) % NBUF);
+        patch_dma(tile_id(i + 2), (i + 2) % NBUF);
         const char* Ps = smem + (i % NBUF) * PBYTES;
         const char* base[FN][3][2];
 #pragma unroll
@@ -573,7 +569,6 @@ __global__ void __launch_bounds__(512, 1) k_c3w64(ConvArgs a, int tiles_w, int t
             for (int j = 0; j < FN; ++j) acc[ii][j] = (pf32x4_t){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < 18; ++s) {
-            if (s == 9 && late) patch_dma(tile_id(i + 2), (i + 2) % NBUF);
             const int tap = s >> 1, hs = s & 1, dy = tap / 3, dx = tap % 3;
             uint4 fb[FN];
 #pragma unroll

@@ -789,10 +789,7 @@ __global__ void __launch_bounds__(512, 1) k_wres1x1(WresArgs a) {
             else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(NST) : "memory");
         }
         // every wave is past tile t - G: its buffer takes tile t + 2G
-        // waves 0-3 issue tile t + 2G's DMA now, waves 4-7 (each SIMD's second wave) after
-        // half of the K-steps, so the two waves of a SIMD do not pause their MFMAs together
-        const bool late = wave & 4, more2 = t + 2 * G < ntiles;
-        if (more2 && !late) dma(t + 2 * G, (k + 2) % NBUF);
+        if (t + 2 * G < ntiles) dma(t + 2 * G, (k + 2) % NBUF);
         const char* X = smem + cur * BUF;
         const char* Rt = X + XB;
         h16_f32x4_t acc[NI][NJ];
@@ -802,7 +799,6 @@ __global__ void __launch_bounds__(512, 1) k_wres1x1(WresArgs a) {
             for (int j = 0; j < NJ; ++j) acc[i][j] = (h16_f32x4_t){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kk = 0; kk < NK; ++kk) {
-            if (kk == NK / 2 && more2 && late) dma(t + 2 * G, (k + 2) % NBUF);
             uint4 bx[NJ];
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
