@@ -708,7 +708,7 @@ __global__ void __launch_bounds__(512, 1) k_wres1x1(WresArgs a) {
     constexpr int BUF = XB + RB, NBUF = 3;
     constexpr int NDX = XB / 1024 / 8, NDR = RB / 1024 / 8;  // DMA instructions per wave
     constexpr int ND = NDX + NDR, NST = (CW / 32) * NJ;      // ... and stores per wave per tile
-    static_assert(NI * NK == 32 && XB % 8192 == 0 && RB % 8192 == 0, "tile shape");
+    static_assert(NI * NK <= 32 && XB % 8192 == 0 && RB % 8192 == 0, "tile shape");
     static_assert(XRB <= 1024 && RRB <= 1024, "row fits one DMA instruction");
     __shared__ __attribute__((aligned(1024))) char smem[NBUF * BUF];
     __shared__ __attribute__((aligned(16))) float sS[BC], sH[BC];
@@ -945,6 +945,9 @@ bool launch_stream1x1(const ConvArgs& a, hipStream_t s, bool f16) {
     if (g_wres && (a.ldy & 7) == 0 && (a.stride == 1 ? a.h == a.ho && a.w_ == a.wo : !res)) {
         if (K == 512 && C == 2048 && res) { launch_wres<512, 32>(a, s, f16); return true; }
         if (K == 256 && C == 1024 && res) { launch_wres<256, 64>(a, s, f16); return true; }
+        // the mod3 block-1 conv3 (128 -> 512 + the projection shortcut): one 512-channel slice,
+        // so its input is read once (the streaming kernel's two slices re-read it)
+        if (K == 128 && C == 512 && res) { launch_wres<128, 64>(a, s, f16); return true; }
         if (g_wres >= 2) {  // the non-residual K = 256 / 512 1x1s (projections, mod4 block-1 conv1)
             if (K == 512 && (C == 256 || C == 1024 || C == 2048) && !res) { launch_wres<512, 32>(a, s, f16); return true; }
             if (K == 256 && (C == 512 || C == 1024) && !res) { launch_wres<256, 64>(a, s, f16); return true; }

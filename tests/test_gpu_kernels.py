@@ -143,6 +143,8 @@ WRES_CASES = [
     (2, 512, 130, 70, 1024, 1, 2, 0, False, True),  # mod4 projection (stride 2), ragged last tile
     (2, 256, 83, 101, 512, 1, 2, 0, False, False),  # mod3 projection (stride 2, odd map)
     (1, 256, 64, 70, 1024, 1, 1, 0, False, True),
+    (1, 128, 63, 71, 512, 1, 1, 0, True, True),     # mod3 last-block conv3 (K = 128): one 512-channel slice
+    (4, 128, 48, 64, 512, 1, 1, 0, True, False),
 ]
 
 
