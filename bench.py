@@ -711,7 +711,9 @@ def main():
             torch.cuda.synchronize()
             try:
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
+                # thread_local: only this thread's calls are checked during the capture (RCCL's
+                # proxy threads may touch the device meanwhile on N > 1)
+                with torch.cuda.graph(g, capture_error_mode="thread_local"):
                     out = state["net"].extract(x)
             except RuntimeError as e:  # capture refused: run eager from here on, and say so
                 print("bench: hipGraph capture failed (%s); extracting with eager launches" % e, file=sys.stderr)
