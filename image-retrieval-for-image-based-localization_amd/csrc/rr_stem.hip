@@ -517,6 +517,7 @@ __global__ void __launch_bounds__(NT) k_stem_pool3(StemArgs a, TAB rt, int tiles
     constexpr int NPAIR = IR * HIC, PPT = (NPAIR + NT - 1) / NT;
     constexpr int PATCH = IR * IC * 8;
     static_assert(PW == 7 * (NT / 64), "one 7-pooled-column block per wave");
+    constexpr int NPRE = 2;  // K-steps of the next odd stem row read ahead (of 7)
     typedef __attribute__((ext_vector_type(2))) float f2;
     __shared__ __attribute__((aligned(16))) char sP[2][PATCH];
     __shared__ float sL[U8 ? 3 * 256 : 1];
@@ -675,20 +676,30 @@ __global__ void __launch_bounds__(NT) k_stem_pool3(StemArgs a, TAB rt, int tiles
         const bool left = pw0 == 0 && wave == 0;
         const int pc0 = 7 * wave + 2 * q;
         const bool st0 = pw0 + pc0 < a.wp, st1 = q < 3 && pw0 + pc0 + 1 < a.wp;
-        auto stem_row = [&](int r, h16_f32x4_t (&acc)[4]) {
+        // the first NPRE K-steps' patch fragments of the next odd stem row are read
+        // before the pooling tail of the current pooled row: their LDS latency
+        // overlaps the tail instead of opening the next row's MFMAs
+        uint4 pre[NPRE];
+        auto preload = [&](int r) {
+            const char* rb = pb + r * (2 * IC * 8);
+#pragma unroll
+            for (int m = 0; m < NPRE; ++m) pre[m] = *reinterpret_cast<const uint4*>(rb + m * IC * 8);
+        };
+        auto stem_row = [&](int r, h16_f32x4_t (&acc)[4], bool use_pre) {
 #pragma unroll
             for (int f = 0; f < 4; ++f) acc[f] = (h16_f32x4_t){0.f, 0.f, 0.f, 0.f};
             const char* rb = pb + r * (2 * IC * 8);
 #pragma unroll
             for (int m = 0; m < 7; ++m) {
-                const uint4 px = *reinterpret_cast<const uint4*>(rb + m * IC * 8);
+                const uint4 px = use_pre && m < NPRE ? pre[m] : *reinterpret_cast<const uint4*>(rb + m * IC * 8);
 #pragma unroll
                 for (int f = 0; f < 4; ++f) acc[f] = H16<HT>::mfma(px, breg[f][m], acc[f]);
             }
         };
         h16_f32x4_t A[4];
         if (active) {
-            stem_row(0, A);
+            stem_row(0, A, false);
+            preload(1);
             if (ph0 == 0) {  // stem row -1: max-pool padding
 #pragma unroll
                 for (int f = 0; f < 4; ++f) A[f] = (h16_f32x4_t){NINF, NINF, NINF, NINF};
@@ -703,13 +714,14 @@ __global__ void __launch_bounds__(NT) k_stem_pool3(StemArgs a, TAB rt, int tiles
                 }
             if (active) {
                 h16_f32x4_t B[4];
-                stem_row(2 * pr + 1, B);
+                stem_row(2 * pr + 1, B, true);
 #pragma unroll
                 for (int f = 0; f < 4; ++f)
 #pragma unroll
                     for (int e = 0; e < 4; ++e) A[f][e] = fmaxf(A[f][e], B[f][e]);  // rows 2pr, 2pr+1
                 h16_f32x4_t C[4];
-                stem_row(2 * pr + 2, C);
+                stem_row(2 * pr + 2, C, false);
+                if (pr + 1 < PH) preload(2 * pr + 3);
                 float p0[4], p1[4];
 #pragma unroll
                 for (int f = 0; f < 4; ++f) {
