@@ -506,6 +506,12 @@ __global__ void __launch_bounds__(NT) k_stem_pool2(StemArgs a, int tiles_w, int 
 // of the normalised value of each byte (x / 255 in IEEE division, then the
 // same normalisation), computed once per block.  Same values as v2 bit for
 // bit when the swapped MFMA accumulates in the same order.
+// first pixel of the 8-B load that carries pixel pair (iw, iw + 1) of an image
+// row of wi pixels: the pair itself inside the row, the row's first / last two
+// pixels where the pair overhangs it (so a pair load never leaves its row when
+// wi >= 2; a 1-pixel row loads its pixel and the next element)
+__device__ __forceinline__ int pair_base(int iw, int wi) { return max(min(iw, wi - 2), 0); }
+
 template <typename HT, bool U8, int NPART, typename TAB = NoTab>
 __global__ void __launch_bounds__(NT) k_stem_pool3(StemArgs a, TAB rt, int tiles_w, int tiles_hw, int ntiles) {
     constexpr bool RG = std::is_same<TAB, RaggedTab>::value;
@@ -598,18 +604,29 @@ __global__ void __launch_bounds__(NT) k_stem_pool3(StemArgs a, TAB rt, int tiles
             const int r = kk / HIC, c = 2 * (kk - r * HIC);
             const int ih = ir0 + r, iw = ic0 + c;
             const bool rok = (unsigned)ih < (unsigned)hi;
-            const int o = (ih * wi + iw) * ESZ;
-            const unsigned off0 = rok && (unsigned)iw < (unsigned)wi ? (unsigned)o : OOBO;
-            const unsigned off1 = rok && (unsigned)(iw + 1) < (unsigned)wi ? (unsigned)(o + ESZ) : OOBO;
+            if constexpr (U8) {  // one byte load per pixel (out of the image: raw 0)
+                const int o = (ih * wi + iw) * ESZ;
+                const unsigned off0 = rok && (unsigned)iw < (unsigned)wi ? (unsigned)o : OOBO;
+                const unsigned off1 = rok && (unsigned)(iw + 1) < (unsigned)wi ? (unsigned)(o + ESZ) : OOBO;
 #pragma unroll
-            for (int ch = 0; ch < 3; ++ch) {
-                const unsigned po = (unsigned)(ch * iplane * ESZ);
-                if constexpr (U8) {
+                for (int ch = 0; ch < 3; ++ch) {
+                    const unsigned po = (unsigned)(ch * iplane * ESZ);
                     pf[uu][2 * ch] = ch * 256 + (int)__builtin_amdgcn_raw_buffer_load_b8(rs, (int)(off0 + po), 0, 0);
                     pf[uu][2 * ch + 1] = ch * 256 + (int)__builtin_amdgcn_raw_buffer_load_b8(rs, (int)(off1 + po), 0, 0);
-                } else {
-                    pf[uu][2 * ch] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(off0 + po), 0, 0));
-                    pf[uu][2 * ch + 1] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(off1 + po), 0, 0));
+                }
+            } else {
+                // float pixels: one 8-B load per pixel pair at pair_base (fill_store
+                // picks the pair's values); for a 1-pixel row the second dword may
+                // pass the buffer end, which the per-dword range check reads as 0
+                // (tools/oob_probe.hip) -- that value is never used
+                const int bw = pair_base(iw, wi);
+                const unsigned offp = rok ? (unsigned)((ih * wi + bw) * ESZ) : OOBO;
+#pragma unroll
+                for (int ch = 0; ch < 3; ++ch) {
+                    const unsigned po = (unsigned)(ch * iplane * ESZ);
+                    const uint2 v2 = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(offp + po), 0, 0));
+                    pf[uu][2 * ch] = __builtin_bit_cast(float, v2.x);
+                    pf[uu][2 * ch + 1] = __builtin_bit_cast(float, v2.y);
                 }
             }
         }
@@ -629,6 +646,13 @@ __global__ void __launch_bounds__(NT) k_stem_pool3(StemArgs a, TAB rt, int tiles
             const bool rok = (unsigned)(ir0 + r) < (unsigned)H;
             const bool ok0 = rok && (unsigned)(ic0 + c) < (unsigned)W;
             const bool ok1 = rok && (unsigned)(ic0 + c + 1) < (unsigned)W;
+            // float pixels (fill_load's pair loads): which loaded value is which
+            // pixel; pixels outside the image row read raw 0 (the ragged batch pad)
+            const int iw = ic0 + c;
+            int wi = W;
+            if constexpr (RG) wi = rt.w[img];
+            const int sh = iw - pair_base(iw, wi);  // -1 / 0 / +1 where a pixel is in the row
+            const bool in0 = (unsigned)iw < (unsigned)wi, in1 = (unsigned)(iw + 1) < (unsigned)wi;
             f2 v[3];
 #pragma unroll
             for (int ch = 0; ch < 3; ++ch) {  // zero padding is applied AFTER normalisation
@@ -636,7 +660,8 @@ __global__ void __launch_bounds__(NT) k_stem_pool3(StemArgs a, TAB rt, int tiles
                 if constexpr (U8) {
                     x = (f2){sL[pf[uu][2 * ch]], sL[pf[uu][2 * ch + 1]]};
                 } else {
-                    x = (f2){pf[uu][2 * ch], pf[uu][2 * ch + 1]};
+                    const float q0 = pf[uu][2 * ch], q1 = pf[uu][2 * ch + 1];
+                    x = (f2){in0 ? (sh > 0 ? q1 : q0) : 0.f, in1 ? (sh < 0 ? q0 : q1) : 0.f};
                     if (a.do_norm) x = (x - (f2){a.mean[ch], a.mean[ch]}) * (f2){a.rstd[ch], a.rstd[ch]};
                 }
                 v[ch] = (f2){ok0 ? x.x : 0.f, ok1 ? x.y : 0.f};

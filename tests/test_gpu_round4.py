@@ -117,6 +117,25 @@ def test_ragged_none_entry_and_long_batch(cuda):
     assert torch.equal(pred["ret_pred"], ref)
 
 
+@pytest.mark.parametrize("u8", [False, True])
+def test_ragged_thin_images(cuda, u8):
+    """images 1-5 pixels wide or high inside a wider batch: the float stem reads pixel
+    pairs with one 8-B load clamped into the image row (a 1-pixel row loads its pixel
+    and the next element), the pad around them reads 0 -- same bits as the padded batch"""
+    from cirtorch.models.GF_net import make_net
+    from cirtorch.models.init import random_init_
+    net = make_net("resnet18", precision="fp16", mean=MEAN, std=STD)
+    random_init_(net, seed=6)
+    net = net.to(cuda).eval()
+    g = torch.Generator(device=cuda).manual_seed(12)
+    sizes = [(64, 96), (40, 1), (33, 2), (20, 3), (1, 50), (2, 5), (64, 95)]
+    if u8:
+        imgs = [torch.randint(0, 256, (3, h, w), generator=g, device=cuda, dtype=torch.uint8) for h, w in sizes]
+    else:
+        imgs = [torch.rand((3, h, w), generator=g, device=cuda) for h, w in sizes]
+    assert torch.equal(net.extract(imgs), net.extract(_padded(imgs)))
+
+
 def test_ragged_stage_maps_equal_padded(cuda):
     """every stage map of the ragged batch equals the padded batch's (fp32 and fp16)"""
     from cirtorch.models.GF_net import make_net
