@@ -457,7 +457,7 @@ def test_stem_pool_before_epilogue_bit_identical(cuda, dt, shape):
     xu = (x * 255).to(torch.uint8)
     outs = {}
     try:
-        for mode in (0, 1, 2):
+        for mode in (0, 1, 2, 3, 4):
             E.check(E.lib().rr_set_tuning(11, mode), "rr_set_tuning")
             outs[mode] = [ops.stem_conv_pool(inp.to(cuda), wpk, scale.to(cuda), shift.to(cuda), leaky=True,
                                              slope=0.01, mean=mean, std=std).float().cpu() for inp in (x, xu)]
@@ -473,6 +473,10 @@ def test_stem_pool_before_epilogue_bit_identical(cuda, dt, shape):
     # v3 (swapped MFMA operands, lane-local pooling, byte table for uint8) == v2
     for b, c in zip(outs[1], outs[2]):
         assert torch.equal(b, c), (b - c).abs().max().item()
+    # v3's patch fill in 2 / 5 parts (the default: 3)
+    for m in (3, 4):
+        for b, c in zip(outs[2], outs[m]):
+            assert torch.equal(b, c), (m, (b - c).abs().max().item())
 
 
 @pytest.mark.parametrize("c_out", [64, 128])

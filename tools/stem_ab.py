@@ -43,6 +43,14 @@ def main():
     outs = {}
     ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     try:
+        # warm-up of every mode and input first: the first timed loop of a process
+        # otherwise runs ~15 % slow (clocks / first touch), whichever mode it is
+        for m in modes:
+            E.check(E.lib().rr_set_tuning(11, m), "rr_set_tuning")
+            for inp in (x, xu):
+                for _ in range(5):
+                    _ops.stem_conv_pool(inp, wpk, scale, shift, mean=mean, std=std)
+        torch.cuda.synchronize()
         for rnd in range(args.rounds):
             for m in modes:
                 E.check(E.lib().rr_set_tuning(11, m), "rr_set_tuning")
