@@ -82,6 +82,9 @@ _SIGS = {
     "rr_cast_f32_bf16": ([_vp, _vp, _ll, _vp], _i),
     "rr_cast_f32_f16": ([_vp, _vp, _ll, _vp], _i),
     "rr_quantize_i8": ([_vp, _ll, _vp, _vp, _vp], _i),
+    "rr_quantize_i8_rows": ([_vp, _i, _i, _vp, _vp, _vp], _i),
+    "rr_knn_topk_checked_i8": ([_vp, _vp, _ll, _vp, _vp, _i, _i, _i, _i, _ll, _vp, _vp, _vp, _sz, _f, _vp, _i, _vp,
+                                _vp, _vp], _i),
 }
 
 _lib = None

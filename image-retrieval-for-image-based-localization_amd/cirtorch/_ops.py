@@ -386,12 +386,14 @@ def knn_workspace_bytes(n_db, nq, d, k, cand=0, dtype=torch.float32):
     return int(E.lib().rr_knn_workspace_bytes(int(n_db), int(nq), int(d), int(k), int(cand), E.dtype_code(dtype)))
 
 
-def knn_topk(db, db_f32, q, q_f32, k, cand=0, idx_offset=0, workspace=None, db_norm_max=None):
-    """db/q: [n, D] rows in the screening dtype (float32, bfloat16 or float16);
+def knn_topk(db, db_f32, q, q_f32, k, cand=0, idx_offset=0, workspace=None, db_norm_max=None, i8_scales=None):
+    """db/q: [n, D] rows in the screening dtype (float32, bfloat16, float16 or int8);
     db_f32/q_f32: the float32 rows used for the exact re-score.
     Returns (scores float64 [Q, k], idx int64 [Q, k]); with db_norm_max (the
     largest database row norm) also int32 [Q] flags: 1 where the screening
-    margin could not be certified (rr_knn_topk_checked)."""
+    margin could not be certified (rr_knn_topk_checked).  int8 screening is
+    certified with i8_scales = (query max|x| [Q] or [1], database max|x| [1])
+    (rr_knn_topk_checked_i8); without them every int8 query is flagged."""
     E.require_gpu(db, db_f32, q, q_f32)
     assert db.dtype == q.dtype and db_f32.dtype == torch.float32 and q_f32.dtype == torch.float32
     for t in (db, db_f32, q, q_f32):
@@ -409,6 +411,15 @@ def knn_topk(db, db_f32, q, q_f32, k, cand=0, idx_offset=0, workspace=None, db_n
                                     workspace.numel(), E.dtype_code(db.dtype), _st()), "rr_knn_topk")
         return out_s, out_i
     unc = torch.empty(nq, dtype=torch.int32, device=db.device)
+    if i8_scales is not None and db.dtype == torch.int8:
+        qa, da = i8_scales
+        assert qa.dtype == torch.float32 and da.dtype == torch.float32 and qa.numel() in (1, nq)
+        E.check(E.lib().rr_knn_topk_checked_i8(E.ptr(db), E.ptr(db_f32), n_db, E.ptr(q), E.ptr(q_f32), nq, d, k,
+                                               int(cand), int(idx_offset), E.ptr(out_s), E.ptr(out_i),
+                                               E.ptr(workspace), workspace.numel(), float(db_norm_max), E.ptr(qa),
+                                               int(qa.numel() == nq and nq > 1), E.ptr(da), E.ptr(unc), _st()),
+                "rr_knn_topk_checked_i8")
+        return out_s, out_i, unc
     E.check(E.lib().rr_knn_topk_checked(E.ptr(db), E.ptr(db_f32), n_db, E.ptr(q), E.ptr(q_f32), nq, d, k, int(cand),
                                         int(idx_offset), E.ptr(out_s), E.ptr(out_i), E.ptr(workspace),
                                         workspace.numel(), E.dtype_code(db.dtype), float(db_norm_max), E.ptr(unc),
@@ -467,17 +478,27 @@ def cast_f16(x):
     return y
 
 
-def quantize_i8(x):
-    """float32 rows -> int8 screening copy: rint(x * 127 / max|x|) clamped to +-127 (one
-    scale for the whole tensor, reduced on the device: no host read-back)."""
+def quantize_i8(x, per_row=False, with_scale=False):
+    """float32 rows -> int8 screening copy: rint(x * 127 / max|x|) clamped to +-127, the
+    scale reduced on the device (no host read-back): one scale for the whole tensor (the
+    database), or with per_row one per row (queries: a query's screened candidates then
+    do not depend on the other queries of its batch).  with_scale: also return the
+    float32 max |x| ([1] or [rows]) -- the certificate's quantisation scale."""
     E.require_gpu(x)
     x = x.contiguous()
     y = torch.empty(x.shape, dtype=torch.int8, device=x.device)
-    if x.numel() % 4:
-        raise RuntimeError("quantize_i8: element count must be a multiple of 4")
-    amax = torch.empty(1, dtype=torch.float32, device=x.device)
-    E.check(E.lib().rr_quantize_i8(E.ptr(x), x.numel(), E.ptr(y), E.ptr(amax), _st()), "rr_quantize_i8")
-    return y
+    if per_row:
+        rows, d = x.shape
+        if d % 4:
+            raise RuntimeError("quantize_i8: row length must be a multiple of 4")
+        amax = torch.empty(rows, dtype=torch.float32, device=x.device)
+        E.check(E.lib().rr_quantize_i8_rows(E.ptr(x), rows, d, E.ptr(y), E.ptr(amax), _st()), "rr_quantize_i8_rows")
+    else:
+        if x.numel() % 4:
+            raise RuntimeError("quantize_i8: element count must be a multiple of 4")
+        amax = torch.empty(1, dtype=torch.float32, device=x.device)
+        E.check(E.lib().rr_quantize_i8(E.ptr(x), x.numel(), E.ptr(y), E.ptr(amax), _st()), "rr_quantize_i8")
+    return (y, amax) if with_scale else y
 
 
 def cast_screen(x, dtype):

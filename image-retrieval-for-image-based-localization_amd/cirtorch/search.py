@@ -22,9 +22,11 @@ import torch.distributed as dist
 from . import _ops
 
 # screening precision of the score GEMM (the final top-k is always the exact float64
-# re-score): int8 = rows quantised with one scale per tensor, exact int32 dot products
-# on v_mfma_i32_16x16x64_i8 (twice the bf16 rate, half the bytes); no certificate
-# (verify=True re-searches every query in float32)
+# re-score): int8 = database rows quantised with one scale per tensor, queries with one
+# per row, exact int32 dot products on v_mfma_i32_16x16x64_i8 (twice the bf16 rate, half
+# the bytes).  Certificates (verify): fp16 / bf16 / fp32 from the rounding error bound,
+# int8 from the quantisation residual bound (~0.02 at D = 2048: on dense random data most
+# int8 queries stay uncertified and are re-searched, so fp16 is the certified default)
 _PREC = {"fp32": torch.float32, "float32": torch.float32, "bf16": torch.bfloat16, "bfloat16": torch.bfloat16,
          "fp16": torch.float16, "float16": torch.float16, "int8": torch.int8}
 
@@ -63,7 +65,11 @@ class KnnIndex:
         self.dim = db_rows.shape[1]
         self.d_pad = _padded_dim(self.dim, self.dtype)
         self.db32 = _pad_cols(db_rows.float().contiguous(), self.d_pad)
-        self.db = _ops.cast_screen(self.db32, self.dtype) if self.db32.shape[0] else self.db32.to(self.dtype)
+        self.db_amax = None   # int8: the database's quantisation scale (max |x|), kept for the certificate
+        if self.dtype == torch.int8 and self.db32.shape[0]:
+            self.db, self.db_amax = _ops.quantize_i8(self.db32, with_scale=True)
+        else:
+            self.db = _ops.cast_screen(self.db32, self.dtype) if self.db32.shape[0] else self.db32.to(self.dtype)
         self.cand = cand
         self.idx_offset = idx_offset
         self._ws = {}   # scratch per stream: searches on different streams never share a slab
@@ -89,6 +95,12 @@ class KnnIndex:
             self._norm_max = float(self.db32.norm(dim=1).max().item()) if self.ntotal else 0.0
         return self._norm_max
 
+    def _screen_queries(self, q32):
+        """float32 query rows -> (screening copy, int8 per-row scales or None)"""
+        if self.dtype == torch.int8:
+            return _ops.quantize_i8(q32, per_row=True, with_scale=True)
+        return _ops.cast_screen(q32, self.dtype), None
+
     def search(self, q_rows, k, verify=False):
         """q_rows [Q, D] -> (scores float64 [Q, k], idx int64 [Q, k]) on the current stream.
         An empty shard (ntotal == 0) returns k (-inf, -1) entries per query, which
@@ -97,47 +109,123 @@ class KnnIndex:
         verify=True certifies the screening margin of every query (the rows left
         out are provably below the returned k-th score given the screening
         dtype's error bound) and re-searches uncertain queries — clusters of
-        near-duplicates tighter than the bf16 / fp16 screening error — with
-        float32 screening and more candidates; this costs one device->host
-        read per search (no graph capture)."""
+        near-duplicates tighter than the screening error — with float32
+        screening and more candidates; this costs one device->host read per
+        search (no graph capture).
+
+        verify="deferred" returns (scores, idx, pending): the same certificate,
+        copied to pinned host memory without a synchronisation; pending.resolve()
+        (later, e.g. once the next batch's work is queued) waits for it and
+        re-searches the uncertain queries in place, returning how many there were."""
         if q_rows.shape[1] != self.dim:
             raise RuntimeError("KnnIndex.search: queries have D=%d, the database D=%d" % (q_rows.shape[1], self.dim))
-        if verify:
-            return self._search_verified(q_rows, k)
         q32 = _pad_cols(q_rows.float().contiguous(), self.d_pad)
         if self.ntotal == 0 or q32.shape[0] == 0:
             s = torch.full((q32.shape[0], k), float("-inf"), dtype=torch.float64, device=q32.device)
-            return s, torch.full((q32.shape[0], k), -1, dtype=torch.int64, device=q32.device)
-        q = _ops.cast_screen(q32, self.dtype)
+            i = torch.full((q32.shape[0], k), -1, dtype=torch.int64, device=q32.device)
+            return (s, i, Pending.done()) if verify == "deferred" else (s, i)
+        if verify:
+            s, i, unc = self.search_checked(q32, k)
+            pend = Pending(unc, lambda bad: self._research(q32, bad, k), s, i)
+            if verify == "deferred":
+                return s, i, pend
+            pend.resolve()
+            return s, i
+        q, _ = self._screen_queries(q32)
         need = _ops.knn_workspace_bytes(self.ntotal, q.shape[0], q.shape[1], k, self.cand, self.dtype)
         return _ops.knn_topk(self.db, self.db32, q, q32, k, cand=self.cand, idx_offset=self.idx_offset,
                              workspace=self._workspace(need, q.device))
 
-
-    def _search_verified(self, q_rows, k):
-        if self.ntotal == 0 or q_rows.shape[0] == 0:
-            return self.search(q_rows, k)
+    def search_checked(self, q_rows, k):
+        """queries [Q, D] -> (scores, idx, int32 [Q] uncertain flags), no synchronisation"""
         q32 = _pad_cols(q_rows.float().contiguous(), self.d_pad)
-        q = _ops.cast_screen(q32, self.dtype)
+        q, qa = self._screen_queries(q32)
         need = _ops.knn_workspace_bytes(self.ntotal, q.shape[0], q.shape[1], k, self.cand, self.dtype)
-        s, i, unc = _ops.knn_topk(self.db, self.db32, q, q32, k, cand=self.cand, idx_offset=self.idx_offset,
-                                  workspace=self._workspace(need, q.device), db_norm_max=self.norm_max())
-        bad = torch.nonzero(unc).flatten()
-        if bad.numel() == 0:
-            return s, i
-        # re-search: float32 screening (error ~d 2^-24), then the largest candidate pool
+        return _ops.knn_topk(self.db, self.db32, q, q32, k, cand=self.cand, idx_offset=self.idx_offset,
+                             workspace=self._workspace(need, q.device), db_norm_max=self.norm_max(),
+                             i8_scales=None if qa is None else (qa, self.db_amax))
+
+    def _research(self, q32, bad, k):
+        """exact top-k of the queries q32[bad] (int64 [n] on the device): float32
+        screening (error ~d 2^-24), then the largest candidate pool"""
+        s, i = None, None
+        sel = torch.arange(bad.numel(), device=bad.device)
         for cand in (0, min(8192, max(1024, 8 * k))):
-            qb = q32[bad].contiguous()
+            qb = q32[bad[sel]].contiguous()
             need = _ops.knn_workspace_bytes(self.ntotal, qb.shape[0], qb.shape[1], k, cand, torch.float32)
             s2, i2, u2 = _ops.knn_topk(self.db32, self.db32, qb, qb, k, cand=cand, idx_offset=self.idx_offset,
                                        workspace=self._workspace(need, qb.device), db_norm_max=self.norm_max())
-            s[bad], i[bad] = s2, i2
+            if s is None:
+                s, i = s2, i2
+            else:
+                s[sel], i[sel] = s2, i2
             keep = torch.nonzero(u2).flatten()
             if keep.numel() == 0:
                 return s, i
-            bad = bad[keep]
-        raise RuntimeError("KnnIndex.search(verify=True): %d queries have more than 8192 near-tied candidates "
-                           "within the float32 screening error" % bad.numel())
+            sel = sel[keep]
+        # more than 8192 rows within the float32 screening error of the k-th score
+        # (exact duplicates of it, say): the full exact ranking of those queries
+        s[sel], i[sel] = self._exact_by_rank(q32[bad[sel]].contiguous(), k)
+        return s, i
+
+    def _exact_by_rank(self, q32, k):
+        """top-k of every row's float64 score by (score desc, index asc) -- rr_rank_full
+        (the k_rescore summation order, stable radix sort), no screening at all; the
+        scores are the same rows re-scored by the top-k pipeline over just those rows
+        (gathered in index order, so its tie order is the global one)"""
+        n, kk = self.ntotal, min(k, self.ntotal)
+        d256 = (self.d_pad + 255) // 256 * 256
+        db = _pad_cols(self.db32, d256)
+        q = _pad_cols(q32, d256)
+        per = max(1, min(65535, RANK_BYTES_MAX // (32 * n)))
+        top = torch.cat([_ops.rank_full(db, q[j:j + per].contiguous())[:, :kk] for j in range(0, q.shape[0], per)])
+        s = torch.full((q32.shape[0], k), float("-inf"), dtype=torch.float64, device=q32.device)
+        i = torch.full((q32.shape[0], k), -1, dtype=torch.int64, device=q32.device)
+        for r in range(q32.shape[0]):
+            rows = torch.sort(top[r]).values
+            sub = KnnIndex(self.db32[rows], "fp32", cand=max(kk, 32))
+            sr, ir = sub.search(q32[r:r + 1], kk)
+            s[r, :kk], i[r, :kk] = sr[0], rows[ir[0]] + self.idx_offset
+        return s, i
+
+
+class Pending:
+    """The certificate of a search, read back later: the int32 flags are copied to
+    pinned host memory on the search's stream and an event is recorded, so the
+    caller is not synchronised until resolve().  resolve() waits for the event and,
+    for the flagged queries, calls research(bad) -> (scores, idx) and writes them
+    into the returned rows; it returns the number of re-searched queries."""
+
+    def __init__(self, unc, research, s, i):
+        self.s, self.i, self.research, self.unc = s, i, research, unc
+        self.ev = None
+        if unc.is_cuda:
+            self.host = torch.empty(unc.shape, dtype=unc.dtype, pin_memory=True)
+            self.host.copy_(unc, non_blocking=True)
+            self.ev = torch.cuda.Event()
+            self.ev.record()
+        else:
+            self.host = unc.clone()
+        self.count = None
+
+    @classmethod
+    def done(cls):
+        p = cls.__new__(cls)
+        p.count = 0
+        return p
+
+    def resolve(self):
+        if self.count is not None:
+            return self.count
+        if self.ev is not None:
+            self.ev.synchronize()
+        bad = torch.nonzero(self.host).flatten()
+        self.count = int(bad.numel())
+        if self.count:
+            bad = bad.to(self.s.device)
+            s2, i2 = self.research(bad)
+            self.s[bad], self.i[bad] = s2, i2
+        return self.count
 
 
 def knn(vecs, qvecs, k, precision="fp32", cand=0):
@@ -213,18 +301,45 @@ class ShardedIndex:
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.merge = merge or _ops.topk_merge
 
-    def search(self, q_rows, k):
-        s, i = self.local.search(q_rows, k)
+    def search(self, q_rows, k, verify=False):
+        """merged top-k of the queries (the same on every rank).  verify=True /
+        "deferred": every shard certifies its own top-k; the flags travel in the
+        same all-gather as the lists, so every rank sees the same uncertain set
+        and re-searches it (each shard in float32, then one more exchange) together."""
+        if not verify:
+            s, i = self.local.search(q_rows, k)
+            return (s, i) if self.world == 1 else self.exchange(s, i, k)
         if self.world == 1:
-            return s, i
-        return self.exchange(s, i, k)
+            return self.local.search(q_rows, k, verify=verify)
+        s, i, pl = self.local.search(q_rows, k, verify="deferred")
+        unc = pl.unc if pl.count is None else torch.zeros(q_rows.shape[0], dtype=torch.int32, device=s.device)
+        s, i, flags = self.exchange(s, i, k, flags=unc)
 
-    def exchange(self, s, i, k):
+        def research(bad):
+            s2, i2 = self.local.search(q_rows[bad], k, verify=True)
+            return self.exchange(s2, i2, k)
+
+        pend = Pending(flags, research, s, i)
+        if verify == "deferred":
+            return s, i, pend
+        pend.resolve()
+        return s, i
+
+    def exchange(self, s, i, k, flags=None):
         """per-shard (score f64, index i64) [Q, k] -> merged [Q, k]: ONE all-gather of
-        the two lists packed as int64 pairs [Q, k, 2] (16 B per entry), then the merge"""
+        the two lists packed as int64 pairs [Q, k, 2] (16 B per entry), then the merge.
+        flags (int32 [Q], optional) ride along as one more pair per query and come back
+        OR-ed over the shards."""
         packed = torch.stack([s.contiguous().view(torch.int64), i], dim=-1)
-        g = all_gather_stacked(packed, self.group)                 # [R, Q, k, 2]
-        return self.merge(g[..., 0].contiguous().view(torch.float64), g[..., 1].contiguous(), k)
+        if flags is not None:
+            extra = torch.zeros((s.shape[0], 1, 2), dtype=torch.int64, device=s.device)
+            extra[:, 0, 0] = flags
+            packed = torch.cat([packed, extra], dim=1)
+        g = all_gather_stacked(packed, self.group)                 # [R, Q, k(+1), 2]
+        ms, mi = self.merge(g[:, :, :k, 0].contiguous().view(torch.float64), g[:, :, :k, 1].contiguous(), k)
+        if flags is None:
+            return ms, mi
+        return ms, mi, g[:, :, k, 0].amax(0).to(torch.int32)
 
 
 def merge_topk(scores, idx, k):

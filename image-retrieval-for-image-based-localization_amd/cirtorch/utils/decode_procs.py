@@ -191,20 +191,42 @@ class ProcDecoder:
                 self.busy.append((event, slots))
 
     def close(self):
+        """terminate the workers, then -- only once no H2D copy can still read the
+        ring -- unpin and release it.  Safe on an error path: copies listed in
+        `busy` are waited for, and so is every other queued copy (a view handed out
+        but never released may have one in flight), before cudaHostUnregister;
+        the segment is unlinked even when unmapping fails because views into it are
+        still alive (BufferError), so /dev/shm is returned when they die."""
         import torch
         try:
             self.pool.terminate()
         except Exception:
             pass
+        with self.lock:
+            busy, self.busy = self.busy, []
+        for ev, _ in busy:
+            try:
+                ev.synchronize()
+            except Exception:
+                pass
         if self.registered:
+            try:
+                if torch.cuda.is_initialized():
+                    torch.cuda.synchronize()
+            except Exception:
+                pass
             try:
                 torch.cuda.cudart().cudaHostUnregister(self._base)
             except Exception:
                 pass
+            self.registered = False
         try:
             self.shm.close()
+        except Exception:   # BufferError: views into the ring are still alive
+            pass
+        try:
             self.shm.unlink()
-        except Exception:
+        except Exception:   # already unlinked
             pass
 
 

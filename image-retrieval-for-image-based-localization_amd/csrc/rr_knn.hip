@@ -700,7 +700,9 @@ __global__ void __launch_bounds__(SEL_THREADS) k_final_sort(const double* __rest
                                                             long long* __restrict__ out_i,
                                                             const uint32_t* __restrict__ sel_thr,
                                                             const float* __restrict__ q32, int d, double delta_scale,
-                                                            int* __restrict__ out_unc) {
+                                                            int* __restrict__ out_unc,
+                                                            const float* __restrict__ i8_qamax, int i8_qstride,
+                                                            const float* __restrict__ i8_dbamax) {
     extern __shared__ __attribute__((aligned(16))) char dyn[];
     double* ks = reinterpret_cast<double*>(dyn);
     int* is = reinterpret_cast<int*>(ks + npow2);
@@ -728,7 +730,23 @@ __global__ void __launch_bounds__(SEL_THREADS) k_final_sort(const double* __rest
             for (int w = 0; w < SEL_WAVES; ++w) tot += red[w];
             const uint32_t thr = sel_thr[q];
             const bool full = k > npow2 || is[k - 1] == 0x7fffffff;  // fewer than k rows: all rows are in
-            const bool ok = thr == 0u || full || (double)funkey(thr) + delta_scale * sqrt(tot) < ks[k - 1];
+            double bound;
+            if (i8_dbamax) {
+                // int8 keys are integer dot products I of q8 = rint(127 q / aq), x8 = rint(127 x / ax):
+                // q.x - s I = s (q8.ex + eq.x8 + eq.ex), s = aq ax / 127^2, residuals |e| <= 1/2 per
+                // element (amax scaling never clamps), so |q.x - s I| <= s E (||q8|| + ||x8|| + E) with
+                // E = sqrt(d) / 2, ||q8|| <= 127 ||q|| / aq + E, ||x8|| <= 127 max||x|| / ax + E; the
+                // f32 key adds |I| 2^-24
+                const double aq = i8_qamax[(long long)q * i8_qstride], ax = *i8_dbamax;
+                const double sc = aq * ax / (127.0 * 127.0);
+                const double E = sqrt((double)d) * 0.50002;
+                const double key = (double)funkey(thr);
+                bound = sc * key + (ax / 127.0 * E * sqrt(tot) + aq / 127.0 * E * delta_scale + 3.0 * sc * E * E +
+                                    sc * fabs(key) * 0x1p-23) * 1.001;
+            } else {
+                bound = (double)funkey(thr) + delta_scale * sqrt(tot);
+            }
+            const bool ok = thr == 0u || full || bound < ks[k - 1];
             out_unc[q] = ok ? 0 : 1;
         }
     }
@@ -818,17 +836,22 @@ size_t rr_knn_workspace_bytes(long long n_db, int nq, int d, int k, int cand, in
     return plan(n_db, nq, k, cand, dtype).total;
 }
 
+static int knn_topk_impl(const void* db, const float* db_f32, long long n_db, const void* q, const float* q_f32,
+                         int nq, int d, int k, int cand, long long idx_offset, double* out_scores, long long* out_idx,
+                         void* workspace, size_t workspace_bytes, int dtype, float db_norm_max, int* out_uncertain,
+                         const float* i8_qamax, int i8_qstride, const float* i8_dbamax, void* stream);
+
 int rr_knn_topk(const void* db, const float* db_f32, long long n_db, const void* q, const float* q_f32, int nq, int d,
                 int k, int cand, long long idx_offset, double* out_scores, long long* out_idx, void* workspace,
                 size_t workspace_bytes, int dtype, void* stream) {
-    return rr_knn_topk_checked(db, db_f32, n_db, q, q_f32, nq, d, k, cand, idx_offset, out_scores, out_idx, workspace,
-                               workspace_bytes, dtype, 1.0f, nullptr, stream);
+    return knn_topk_impl(db, db_f32, n_db, q, q_f32, nq, d, k, cand, idx_offset, out_scores, out_idx, workspace,
+                         workspace_bytes, dtype, 1.0f, nullptr, nullptr, 0, nullptr, stream);
 }
 
-int rr_knn_topk_checked(const void* db, const float* db_f32, long long n_db, const void* q, const float* q_f32, int nq,
-                        int d, int k, int cand, long long idx_offset, double* out_scores, long long* out_idx,
-                        void* workspace, size_t workspace_bytes, int dtype, float db_norm_max, int* out_uncertain,
-                        void* stream) {
+static int knn_topk_impl(const void* db, const float* db_f32, long long n_db, const void* q, const float* q_f32,
+                         int nq, int d, int k, int cand, long long idx_offset, double* out_scores, long long* out_idx,
+                         void* workspace, size_t workspace_bytes, int dtype, float db_norm_max, int* out_uncertain,
+                         const float* i8_qamax, int i8_qstride, const float* i8_dbamax, void* stream) {
     if (n_db <= 0 || nq <= 0 || k <= 0) return fail(RR_EINVAL, "rr_knn_topk: empty problem");
     if (n_db > 0x7fffffffll) return fail(RR_EINVAL, "rr_knn_topk: shard rows must fit int32 (shard the database)");
     if (dtype != RR_BF16 && dtype != RR_F32 && dtype != RR_F16 && dtype != RR_I8)
@@ -942,14 +965,35 @@ int rr_knn_topk_checked(const void* db, const float* db_f32, long long n_db, con
     // screening error bound per unit ||q|| ||x||: input rounding of both
     // operands (bf16 2^-9, fp16 2^-11 relative each; products exact in f32)
     // plus f32 accumulation over d terms (d 2^-24)
-    // int8 scores are integer dot products (no common scale with the exact scores):
-    // no certificate, every query with more than k rows is flagged
+    // int8 scores are integer dot products: certified only through rr_knn_topk_checked_i8,
+    // which passes the quantisation scales (without them every query with more than k rows is flagged)
     const double in_eps = dtype == RR_BF16 ? 0x1p-8 + 0x1p-17 : dtype == RR_F16 ? 0x1p-10 + 0x1p-21 : 0.0;
-    const double delta_scale = dtype == RR_I8 ? (double)INFINITY
+    // (int8 with its scales: k_final_sort's own bound, delta_scale = max ||x||; without them: no certificate)
+    const bool i8_cert = dtype == RR_I8 && i8_qamax && i8_dbamax;
+    const double delta_scale = dtype == RR_I8 ? (i8_cert ? (db_norm_max > 0.f ? (double)db_norm_max : 1.0) : (double)INFINITY)
                                               : (in_eps + d * 0x1p-24) * 1.001 * (db_norm_max > 0.f ? db_norm_max : 1.0);
     hipLaunchKernelGGL(k_final_sort, dim3(nq), dim3(SEL_THREADS), fin_lds, s, fin_s, fin_i, p.npow2, k, idx_offset,
-                       out_scores, out_idx, sel_thr, q_f32, d, delta_scale, out_uncertain);
+                       out_scores, out_idx, sel_thr, q_f32, d, delta_scale, out_uncertain, i8_cert ? i8_qamax : nullptr,
+                       i8_qstride, i8_cert ? i8_dbamax : nullptr);
     return check_launch("rr_knn_topk");
+}
+
+int rr_knn_topk_checked(const void* db, const float* db_f32, long long n_db, const void* q, const float* q_f32, int nq,
+                        int d, int k, int cand, long long idx_offset, double* out_scores, long long* out_idx,
+                        void* workspace, size_t workspace_bytes, int dtype, float db_norm_max, int* out_uncertain,
+                        void* stream) {
+    return knn_topk_impl(db, db_f32, n_db, q, q_f32, nq, d, k, cand, idx_offset, out_scores, out_idx, workspace,
+                         workspace_bytes, dtype, db_norm_max, out_uncertain, nullptr, 0, nullptr, stream);
+}
+
+int rr_knn_topk_checked_i8(const void* db, const float* db_f32, long long n_db, const void* q, const float* q_f32,
+                           int nq, int d, int k, int cand, long long idx_offset, double* out_scores, long long* out_idx,
+                           void* workspace, size_t workspace_bytes, float db_norm_max, const float* q_amax,
+                           int q_amax_per_row, const float* db_amax, int* out_uncertain, void* stream) {
+    if (!q_amax || !db_amax || !out_uncertain) return fail(RR_EINVAL, "rr_knn_topk_checked_i8: null scale / flags");
+    return knn_topk_impl(db, db_f32, n_db, q, q_f32, nq, d, k, cand, idx_offset, out_scores, out_idx, workspace,
+                         workspace_bytes, RR_I8, db_norm_max, out_uncertain, q_amax, q_amax_per_row ? 1 : 0, db_amax,
+                         stream);
 }
 
 int rr_topk_merge(const double* in_scores, const long long* in_idx, int r, int nq, int k_in, int k, double* out_scores,

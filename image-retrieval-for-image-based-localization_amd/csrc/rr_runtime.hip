@@ -346,6 +346,33 @@ __global__ void __launch_bounds__(256) k_cast_f32_i8(const float* __restrict__ x
     }
 }
 
+// Per-row int8 screening copy (queries): one wave per row, amax_rows[r] = max |x_r|,
+// y_r = clamp(rint(x_r * 127 / amax_rows[r]), -127, 127).  A positive per-row
+// scale leaves each query's ranking unchanged, so a query's screened candidates
+// no longer depend on the other queries of its batch.
+__global__ void __launch_bounds__(256) k_quantize_i8_rows(const float* __restrict__ x, int rows, int d,
+                                                          int8_t* __restrict__ y, float* __restrict__ amax_rows) {
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= rows) return;
+    const float* xr = x + (long long)r * d;
+    float m = 0.f;
+    for (int i = lane * 4; i < d; i += 256) {
+        const float4 v = *reinterpret_cast<const float4*>(xr + i);
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+    m = wave_max(m);
+    const float sc = m > 0.f ? 127.f / m : 1.f;
+    auto q = [&](float v) { return (int)fminf(fmaxf(rintf(v * sc), -127.f), 127.f); };
+    for (int i = lane * 4; i < d; i += 256) {
+        const float4 v = *reinterpret_cast<const float4*>(xr + i);
+        const unsigned w = (unsigned)(q(v.x) & 255) | ((unsigned)(q(v.y) & 255) << 8) |
+                           ((unsigned)(q(v.z) & 255) << 16) | ((unsigned)(q(v.w) & 255) << 24);
+        *reinterpret_cast<unsigned*>(y + (long long)r * d + i) = w;
+    }
+    if (lane == 0) amax_rows[r] = m;
+}
+
 static inline unsigned cast_blocks(long long n) {
     const long long b = (n + 1023) / 1024;       // 256 threads x 4 elements
     return (unsigned)(b < (1ll << 20) ? (b > 0 ? b : 1) : (1ll << 20));
@@ -527,6 +554,16 @@ int rr_quantize_i8(const float* x, long long n, void* y, float* amax_dev, void* 
     hipLaunchKernelGGL(k_cast_f32_i8, dim3(cast_blocks(n)), dim3(256), 0, s, x, n, (const unsigned*)amax_dev,
                        (int8_t*)y);
     return check_launch("rr_quantize_i8");
+}
+
+int rr_quantize_i8_rows(const float* x, int rows, int d, void* y, float* amax_rows, void* stream) {
+    if (rows <= 0) return RR_OK;
+    if (!x || !y || !amax_rows) return fail(RR_EINVAL, "rr_quantize_i8_rows: null pointer");
+    if (d <= 0 || d % 4 || ((uintptr_t)x & 15) || ((uintptr_t)y & 3))
+        return fail(RR_EINVAL, "rr_quantize_i8_rows: d % 4, alignment");
+    hipLaunchKernelGGL(k_quantize_i8_rows, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, as_stream(stream), x, rows,
+                       d, (int8_t*)y, amax_rows);
+    return check_launch("rr_quantize_i8_rows");
 }
 
 int rr_cast_f32_bf16(const float* x, void* y, long long n, void* stream) {

@@ -243,6 +243,19 @@ int rr_knn_topk_checked(const void* db, const float* db_f32, long long n_db,
                         void* workspace, size_t workspace_bytes, int dtype, float db_norm_max,
                         int* out_uncertain, void* stream);
 
+/* The certificate for int8 screening (rr_quantize_i8 database, rr_quantize_i8_rows
+ * or rr_quantize_i8 queries): q_amax = the queries' max |x| (one per row when
+ * q_amax_per_row, else one for all), db_amax = the database's; the bound is the
+ * quantisation residual bound s E (||q8|| + ||x8|| + E), s = aq ax / 127^2,
+ * E = sqrt(d) / 2 — ~0.02 at d = 2048, so on dense random data most queries stay
+ * uncertified (re-search them), while well-separated top-k certify. */
+int rr_knn_topk_checked_i8(const void* db, const float* db_f32, long long n_db,
+                           const void* q, const float* q_f32, int nq, int d, int k, int cand,
+                           long long idx_offset, double* out_scores, long long* out_idx,
+                           void* workspace, size_t workspace_bytes, float db_norm_max,
+                           const float* q_amax, int q_amax_per_row, const float* db_amax,
+                           int* out_uncertain, void* stream);
+
 /* Merge R per-shard top-k lists per query into one top-k by (score desc,
  * index asc).  in_*: [R][nq][k_in]; out_*: [nq][k].  Used after the RCCL
  * all-gather of per-shard results.  k_in*R <= 4096. */
@@ -357,13 +370,17 @@ int rr_set_tuning(int key, int value);
  * depends only on (seed, i0 + i), so shards generate identical rows. */
 int rr_fill_unit_rows(float* out, long long rows, int d, unsigned long long seed,
                       long long row0, void* stream);
-/* float32 -> bf16 (round to nearest even). */
 /* int8 screening copy of float32 rows for rr_knn_topk(dtype RR_I8): y = clamp(rint(x * 127 / amax),
  * -127, 127) with amax = max |x| over all n elements, reduced on the device into amax_dev (one float of
  * caller scratch; no host synchronisation).  The screening scores are then exact int32 dot products of
  * the quantised rows (v_mfma_i32_16x16x64_i8, twice the bf16 MFMA rate, half the bf16 bytes); the final
  * top-k is the exact float64 re-score of the candidates, as for every screening dtype. */
 int rr_quantize_i8(const float* x, long long n, void* y, float* amax_dev, void* stream);
+/* Per-row int8 copy (queries): amax_rows[r] = max |x_r|, y_r = clamp(rint(x_r * 127 / amax_rows[r]),
+ * -127, 127); x [rows][d] float32, d % 4 == 0.  A query's screened candidates then do not depend on
+ * the other queries of its batch. */
+int rr_quantize_i8_rows(const float* x, int rows, int d, void* y, float* amax_rows, void* stream);
+/* float32 -> bf16 (round to nearest even). */
 int rr_cast_f32_bf16(const float* x, void* y, long long n, void* stream);
 /* float32 -> fp16 (IEEE binary16, round to nearest even). */
 int rr_cast_f32_f16(const float* x, void* y, long long n, void* stream);

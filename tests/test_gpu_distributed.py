@@ -26,7 +26,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n, d, q, k, prec, ret):
+def _worker(rank, world, port, n, d, q, k, prec, ret, verify=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import sys
@@ -47,9 +47,14 @@ def _worker(rank, world, port, n, d, q, k, prec, ret):
         # each rank extracts its own queries, then all of them are gathered (bench.py step)
         qs = _ops.fill_unit_rows(q * world, d, seed=0x5EED2, device=dev)[rank * q:(rank + 1) * q].contiguous()
         qa = all_gather_stacked(qs).reshape(world * q, d)
-        s, i = idx.search(qa, k)
+        if verify == "deferred":
+            s, i, pend = idx.search(qa, k, verify="deferred")
+            n_re = pend.resolve()
+        else:
+            s, i = idx.search(qa, k, verify=verify)
+            n_re = -1
         torch.cuda.synchronize()
-        ret[rank] = (s.cpu().numpy(), i.cpu().numpy())
+        ret[rank] = (s.cpu().numpy(), i.cpu().numpy(), n_re)
     finally:
         dist.destroy_process_group()
 
@@ -70,11 +75,38 @@ def test_sharded_real_kernels_equal_single_search(cuda, world, n, prec):
     s1, i1 = KnnIndex(db, prec).search(qa, k)
     s1, i1 = s1.cpu().numpy(), i1.cpu().numpy()
     for r in range(world):
-        s, i = ret[r]
+        s, i, _ = ret[r]
         np.testing.assert_array_equal(i, i1)
         np.testing.assert_array_equal(s, s1)
     if n < k:
         assert (i1[:, n:] == -1).all()
+
+
+@pytest.mark.parametrize("world,n,prec,verify", [(2, 70001, "fp16", "deferred"), (2, 70001, "int8", "deferred"),
+                                                 (3, 40000, "bf16", True)])
+def test_sharded_real_kernels_certified(cuda, world, n, prec, verify):
+    """The certified sharded search: each shard's certificate travels in the
+    top-k all-gather, every rank re-searches the same uncertain queries and
+    exchanges again -- the merged result equals the exact oracle on every rank,
+    and every rank reports the same re-searched count."""
+    from cirtorch import _ops
+    from oracle import ops
+    d, q, k = 256, 3, 50
+    ctx = mp.get_context("spawn")
+    mgr = ctx.Manager()
+    ret = mgr.dict()
+    mp.start_processes(_worker, args=(world, _free_port(), n, d, q, k, prec, ret, verify), nprocs=world, join=True,
+                       start_method="spawn")
+    db = _ops.fill_unit_rows(n, d, seed=0x5EED1, device=cuda).cpu().numpy()
+    qa = _ops.fill_unit_rows(q * world, d, seed=0x5EED2, device=cuda).cpu().numpy()
+    ref_s, ref_i = ops.topk_exact(db, qa, k)
+    counts = set()
+    for r in range(world):
+        s, i, n_re = ret[r]
+        np.testing.assert_array_equal(i, ref_i)
+        np.testing.assert_allclose(s, ref_s, rtol=0, atol=1e-12)
+        counts.add(n_re)
+    assert len(counts) == 1
 
 
 def test_c_abi_rccl_single_rank_merge(cuda):

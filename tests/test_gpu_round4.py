@@ -22,7 +22,7 @@ from conftest import cosines, golden
 pytestmark = pytest.mark.gpu
 
 FP32_COS = 1 - 1e-4
-FP16_COS = 1 - 5e-4
+FP16_COS = 1 - 1e-4  # the north-star bar the fp16 headline claims
 BF16_COS = 1 - 2e-3
 MEAN, STD = [0.485, 0.456, 0.406], [0.229, 0.224, 0.225]
 
