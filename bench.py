@@ -62,6 +62,10 @@ def parse():
                          "re-searched in float32) and the top-k is the exact float64 re-score.  fp16 (default): "
                          "the bound (~1e-3) certifies random 2048-d data; int8's residual bound (~0.02) does not, "
                          "so int8 is timed uncertified as the knn.int8_screen sub-line")
+    ap.add_argument("--query-batch", type=int, default=1024,
+                    help="queries per rank per search: the step's descriptors are searched in batches of this many "
+                         "(the reference ranks all extracted queries in one np.dot, scripts/test.py:236-248); every "
+                         "batch, the last one flushed, is searched inside the timed region.  0 = one search per step")
     ap.add_argument("--db-rows", type=int, default=1_000_000)
     ap.add_argument("--dim", type=int, default=2048)
     ap.add_argument("--k", type=int, default=100)
@@ -687,10 +691,11 @@ def main():
     state = {"net": net, "index": index}
 
     def match(desc):
-        """the certified search of the step's queries: (scores, idx, pending certificate)"""
+        """the certified search of a batch of this rank's queries (D x n) and, for N > 1, every
+        other rank's: (scores, idx, pending certificate)"""
         q = desc.t().contiguous()
         if world > 1:
-            q = all_gather_stacked(q).reshape(world * B, q.shape[1])
+            q = all_gather_stacked(q).reshape(world * q.shape[0], q.shape[1])
         if args.search_cus <= 0:
             return state["index"].search(q, args.k, verify="deferred")
         # the cap is read when a kernel is launched: only the search's launches see it
@@ -707,18 +712,39 @@ def main():
         with torch.cuda.stream(match_stream):
             return res[2].resolve()
 
+    QB = 0 if args.query_batch <= 0 else max(B, args.query_batch // B * B)  # queries per rank per search
+    queued = []   # this rank's extracted, not yet searched descriptors (D x B each)
+
+    def search_queued():
+        """launch the certified search of the queued descriptors on the search stream"""
+        desc = queued[0] if len(queued) == 1 else torch.cat(queued, dim=1)
+        queued.clear()
+        if match_stream is main_stream:
+            return match(desc)
+        ready = torch.cuda.Event()
+        ready.record(main_stream)
+        with torch.cuda.stream(match_stream):
+            match_stream.wait_event(ready)
+            desc.record_stream(match_stream)
+            return match(desc)
+
     def run_steps(n, record):
-        """n steps, each step's certificate resolved after the next step is queued; the
-        last one before returning (inside the caller's timed region)"""
-        prev, requeried = None, 0
-        for _ in range(n):
-            res = step(record)
-            if prev is not None:
-                requeried += resolve(prev)
-            prev = res
+        """n steps; a search is launched whenever QB queries are queued (every step with
+        --query-batch 0) and the rest are flushed at the end; each search's certificate is
+        resolved after the next search is queued, the last one before returning (inside
+        the caller's timed region) -> (re-searched queries, searches)"""
+        prev, requeried, searches = None, 0, 0
+        for i in range(n):
+            queued.append(extract_all(record))
+            if QB == 0 or len(queued) * B >= QB or i == n - 1:
+                res = search_queued()
+                searches += 1
+                if prev is not None:
+                    requeried += resolve(prev)
+                prev = res
         if prev is not None:
             requeried += resolve(prev)
-        return requeried
+        return requeried, searches
 
     EB = max(1, min(args.extract_batch, B))
 
@@ -763,27 +789,13 @@ def main():
                 ev_pairs.append((e0, e1))
         return descs[0] if len(descs) == 1 else torch.cat(descs, dim=1)
 
-    def step(record):
-        """extract the step's images on the main stream, then one top-k search
-        of all of them; with --overlap the match (memory-bound kNN + RCCL) runs
-        on a second stream, overlapping the next step's extraction."""
-        desc = extract_all(record)                  # D x B (on-device, fp32)
-        if match_stream is main_stream:
-            return match(desc)
-        ready = torch.cuda.Event()
-        ready.record(main_stream)
-        with torch.cuda.stream(match_stream):
-            match_stream.wait_event(ready)
-            desc.record_stream(match_stream)
-            return match(desc)
-
     with torch.no_grad():
         run_steps(args.warmup, False)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
-        step_requeried = run_steps(args.steps, True)
+        step_requeried, step_searches = run_steps(args.steps, True)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -805,7 +817,7 @@ def main():
             if world > 1:
                 dist.barrier()
             ta = time.perf_counter()
-            alt_requeried = run_steps(args.alt_steps, False)
+            alt_requeried, _ = run_steps(args.alt_steps, False)
             torch.cuda.synchronize()
             if world > 1:
                 dist.barrier()
@@ -1090,18 +1102,21 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "requeried": step_requeried,
+        "searches": step_searches,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": args.precision,
         "data": "synthetic (U[0,1) images, random-init weights, counter-hash N(0,1) unit DB rows)",
-        "config": {"workload": "%s-GeM+whiten %s extract %dx%d, B=%d/GPU (chains of %d), then top-%d cosine kNN of "
-                               "all %d queries vs %d x %d DB sharded over %d GPU(s) (%s screening, certified per query, "
-                               "exact float64 re-score)%s"
-                               % (args.arch, args.precision, W, H, B, EB, args.k, B * world, args.db_rows, args.dim,
-                                  world, args.screen, "; each step's search on a second stream beside the next step's extraction"
-                                  if args.overlap else ""),
-                   "global_batch": B * world, "extract_batch": EB, "image": [3, H, W], "db_rows": args.db_rows,
+        "config": {"workload": "%s-GeM+whiten %s extract %dx%d, B=%d/GPU per step (chains of %d); every extracted "
+                               "image is a query: top-%d cosine kNN vs %d x %d DB sharded over %d GPU(s) (%s screening, "
+                               "certified per query, exact float64 re-score), %s, all inside the timed region%s"
+                               % (args.arch, args.precision, W, H, B, EB, args.k, args.db_rows, args.dim, world,
+                                  args.screen, ("searched in batches of %d queries per GPU (%d gathered per search; the "
+                                                "last batch flushed)" % (QB, QB * world)) if QB else
+                                  "searched every step (%d queries gathered)" % (B * world),
+                                  "; the searches on a second stream beside the extraction" if args.overlap else ""),
+                   "global_batch": B * world, "query_batch": QB * world if QB else B * world, "extract_batch": EB, "image": [3, H, W], "db_rows": args.db_rows,
                    "dim": args.dim,
                    "k": args.k, "parallelism": "dp%d (images) x db-shard%d" % (world, world),
                    "launch": "extractor chains replayed as hipGraphs" if args.graph else "eager launches"},

@@ -454,6 +454,62 @@ __device__ void bitonic_best_first(double* ks, I* is, int n) {
 // slots are (key 0, index -1) in the unstaged form; one such entry is appended
 // when any exists, so the K-th key (and thereby sel_thr) and the selected set
 // are the same.  Indices are read from the slot array for the taken keys only.
+// Re-score cut (certified): with delta = the screening error bound of the query
+// (delta_scale * ||q||), every candidate's exact score lies within delta of its
+// screening key, so the k best keys have exact scores >= t_k - delta (t_k = the
+// k-th largest candidate key) and so does the exact k-th score; a candidate with
+// key < t_k - 2 delta has an exact score < t_k - delta, strictly below it -- it
+// cannot be in the top k, and k_rescore skips its float32 row (-inf).
+// prune_thr[q] = t_k - 2 delta, or -inf when fewer than k candidates are valid.
+__device__ void rescore_cut(const uint32_t* __restrict__ keys, int KC, int k, const float* __restrict__ qr, int d,
+                            double delta_scale, int* smi, float* __restrict__ out) {
+    __shared__ double red[SEL_WAVES];
+    __shared__ int nvs[SEL_WAVES];
+    __shared__ uint32_t tk_s;
+    uint32_t* lk = reinterpret_cast<uint32_t*>(smi);  // KC <= SEL_THREADS keys (TOPK_BINS >= SEL_THREADS)
+    __syncthreads();  // this block's sel_k stores are visible to all its threads; smi is free
+    const int tid = threadIdx.x;
+    const bool small = KC <= SEL_THREADS;             // block-uniform
+    const uint32_t mine = tid < KC && small ? keys[tid] : 0u;
+    if (small && tid < KC) lk[tid] = mine;
+    if (tid == 0) tk_s = 0u;
+    double ss = 0.0;
+    for (int t = tid; t < d; t += SEL_THREADS) ss += (double)qr[t] * qr[t];
+    ss = wave_sum_d(ss);
+    int nv = mine != 0u;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) nv += __shfl_xor(nv, o, 64);
+    if ((tid & 63) == 0) {
+        red[tid >> 6] = ss;
+        nvs[tid >> 6] = nv;
+    }
+    __syncthreads();
+    int tot_nv = 0;
+    double tot = 0.0;
+    for (int w = 0; w < SEL_WAVES; ++w) { tot_nv += nvs[w]; tot += red[w]; }
+    if (!small || tot_nv <= k) {  // block-uniform: no cut
+        if (tid == 0) *out = -INFINITY;
+        return;
+    }
+    // t_k = the k-th largest valid key: the key x with #{> x} < k <= #{>= x}
+    if (mine != 0u) {
+        int gt = 0, ge = 0;
+        for (int i = 0; i < KC; ++i) {
+            const uint32_t v = lk[i];
+            gt += v > mine;
+            ge += v >= mine;
+        }
+        if (gt < k && k <= ge) tk_s = mine;  // every writer writes the same value
+    }
+    __syncthreads();
+    if (tid == 0) {
+        const double cut = (double)funkey(tk_s) - 2.0 * delta_scale * sqrt(tot) * 1.0001;
+        float f = (float)cut;
+        if ((double)f > cut) f = nextafterf(f, -INFINITY);  // round the cut down
+        *out = f;
+    }
+}
+
 constexpr int FSEL_CAP = 12288;   // staged keys (48 KiB): ~4.2k occupied for 1M rows at k = 100
 constexpr int FSEL_MAXCH = 1024;  // chunk offsets (4 KiB)
 constexpr size_t FSEL_LDS = (size_t)(FSEL_CAP + FSEL_MAXCH + 1) * 4;
@@ -461,7 +517,9 @@ __global__ void __launch_bounds__(SEL_THREADS) k_final_select(const uint32_t* __
                                                               const int* __restrict__ cand_i,
                                                               const int* __restrict__ cnt, int nchunks, int KC,
                                                               uint32_t* __restrict__ sel_k, int* __restrict__ sel_i,
-                                                              uint32_t* __restrict__ sel_thr, int stage) {
+                                                              uint32_t* __restrict__ sel_thr, int stage, int k,
+                                                              const float* __restrict__ q32, int d, double delta_scale,
+                                                              float* __restrict__ prune_thr) {
     __shared__ int smi[TOPK_BINS + 64];
     extern __shared__ __attribute__((aligned(16))) char dyn[];
     const int q = blockIdx.x;
@@ -512,6 +570,8 @@ __global__ void __launch_bounds__(SEL_THREADS) k_final_select(const uint32_t* __
             const uint32_t thr = block_topk<false, true>([&](int i) { return lk[i]; }, gi, total + (pad ? 1 : 0), KC,
                                                          sel_k + (long long)q * KC, sel_i + (long long)q * KC, smi);
             if (threadIdx.x == 0) sel_thr[q] = thr;
+            if (prune_thr) rescore_cut(sel_k + (long long)q * KC, KC, k, q32 + (long long)q * d, d, delta_scale, smi,
+                                       prune_thr + q);
             return;
         }
     }
@@ -525,6 +585,8 @@ __global__ void __launch_bounds__(SEL_THREADS) k_final_select(const uint32_t* __
     // every row outside the KC candidates has a screening key <= thr: a chunk's
     // own KC-th key, the running threshold and the pool's KC-th key are all <= it
     if (threadIdx.x == 0) sel_thr[q] = thr;
+    if (prune_thr) rescore_cut(sel_k + (long long)q * KC, KC, k, q32 + (long long)q * d, d, delta_scale, smi,
+                               prune_thr + q);
 }
 
 // After the prefix chunks: tau[q] = the KC-th largest key of the whole prefix
@@ -658,13 +720,16 @@ __global__ void __launch_bounds__(SEL_THREADS) k_slot_fixup(const T* __restrict_
 // order and a butterfly reduction -> bit-reproducible on any sharding.
 __global__ void __launch_bounds__(256) k_rescore(const int* __restrict__ sel_i, int KC, int npow2,
                                                  const float* __restrict__ db32, const float* __restrict__ q32, int d,
-                                                 double* __restrict__ fin_s, int* __restrict__ fin_i) {
+                                                 double* __restrict__ fin_s, int* __restrict__ fin_i,
+                                                 const uint32_t* __restrict__ sel_k, const float* __restrict__ prune_thr) {
     const int q = blockIdx.y, lane = threadIdx.x & 63;
     const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (j >= npow2) return;
     const int idx = j < KC ? sel_i[(long long)q * KC + j] : -1;
+    // a candidate below the certified cut (rescore_cut) cannot be in the top k: no row read
+    const bool cut = prune_thr && idx >= 0 && funkey(sel_k[(long long)q * KC + j]) < prune_thr[q];
     double sc = -INFINITY;
-    if (idx >= 0) {
+    if (idx >= 0 && !cut) {
         const float* dr = db32 + (long long)idx * d;
         const float* qr = q32 + (long long)q * d;
         double acc = 0.0;
@@ -790,7 +855,7 @@ static int pow2_at_least(int v) {
 struct KnnPlan {
     int L, nchunks, G, KC, npow2;
     long long S;
-    size_t slab_bytes, cand_bytes, sel_bytes, fin_bytes, tau_bytes, cnt_bytes, total;  // tau_bytes: tau + sel_thr
+    size_t slab_bytes, cand_bytes, sel_bytes, fin_bytes, tau_bytes, cnt_bytes, total;  // tau_bytes: tau + sel_thr + prune_thr
 };
 
 static int default_cand(int k, int dtype) {
@@ -817,7 +882,7 @@ static KnnPlan plan(long long n_db, int nq, int k, int cand, int dtype) {
     p.cand_bytes = (size_t)nq * p.nchunks * p.KC * 4;
     p.sel_bytes = ((size_t)nq * p.KC * 4 + 255) / 256 * 256;
     p.fin_bytes = ((size_t)nq * p.npow2 * 8 + 255) / 256 * 256 + ((size_t)nq * p.npow2 * 4 + 255) / 256 * 256;
-    p.tau_bytes = ((size_t)nq * 8 + 255) / 256 * 256;
+    p.tau_bytes = ((size_t)nq * 12 + 255) / 256 * 256;  // tau, sel_thr, prune_thr
     p.cnt_bytes = ((size_t)nq * p.nchunks * 4 + 255) / 256 * 256;
     p.total = p.slab_bytes + 2 * ((p.cand_bytes + 255) / 256 * 256) + 2 * p.sel_bytes + p.fin_bytes + p.tau_bytes +
               p.cnt_bytes;
@@ -876,6 +941,7 @@ static int knn_topk_impl(const void* db, const float* db_f32, long long n_db, co
     int* fin_i = (int*)(fws + 2 * p.sel_bytes + ((size_t)nq * p.npow2 * 8 + 255) / 256 * 256);
     uint32_t* tau = (uint32_t*)(fws + 2 * p.sel_bytes + p.fin_bytes);
     uint32_t* sel_thr = tau + nq;
+    float* prune_thr = reinterpret_cast<float*>(sel_thr + nq);
     int* cnt = (int*)(fws + 2 * p.sel_bytes + p.fin_bytes + p.tau_bytes);
 
     static bool attr_done = false;
@@ -955,13 +1021,6 @@ static int knn_topk_impl(const void* db, const float* db_f32, long long n_db, co
     }
     const size_t fin_lds = (size_t)p.npow2 * 12;
     if (fin_lds > 160 * 1024 - 4096) return fail(RR_EINVAL, "rr_knn_topk: candidate set exceeds LDS");
-    // RR_KNN_FSEL=0: the unstaged final select (A/B)
-    static const int fsel = getenv("RR_KNN_FSEL") ? atoi(getenv("RR_KNN_FSEL")) : 1;
-    const int stage = fsel && p.nchunks <= FSEL_MAXCH;
-    hipLaunchKernelGGL(k_final_select, dim3(nq), dim3(SEL_THREADS), stage ? FSEL_LDS : 0, s, cand_k, cand_i, cnt,
-                       p.nchunks, p.KC, sel_k, sel_i, sel_thr, stage);
-    hipLaunchKernelGGL(k_rescore, dim3((p.npow2 + 3) / 4, nq), dim3(256), 0, s, sel_i, p.KC, p.npow2, db_f32, q_f32, d,
-                       fin_s, fin_i);
     // screening error bound per unit ||q|| ||x||: input rounding of both
     // operands (bf16 2^-9, fp16 2^-11 relative each; products exact in f32)
     // plus f32 accumulation over d terms (d 2^-24)
@@ -970,8 +1029,19 @@ static int knn_topk_impl(const void* db, const float* db_f32, long long n_db, co
     const double in_eps = dtype == RR_BF16 ? 0x1p-8 + 0x1p-17 : dtype == RR_F16 ? 0x1p-10 + 0x1p-21 : 0.0;
     // (int8 with its scales: k_final_sort's own bound, delta_scale = max ||x||; without them: no certificate)
     const bool i8_cert = dtype == RR_I8 && i8_qamax && i8_dbamax;
-    const double delta_scale = dtype == RR_I8 ? (i8_cert ? (db_norm_max > 0.f ? (double)db_norm_max : 1.0) : (double)INFINITY)
-                                              : (in_eps + d * 0x1p-24) * 1.001 * (db_norm_max > 0.f ? db_norm_max : 1.0);
+    const double nm = db_norm_max > 0.f ? (double)db_norm_max : 1.0;
+    const double delta_scale = dtype == RR_I8 ? (i8_cert ? nm : (double)INFINITY) : (in_eps + d * 0x1p-24) * 1.001 * nm;
+    // the certified re-score cut (16/32-bit screens, whose keys are scores): only with a
+    // known database norm bound (the checked entry points), RR_KNN_CUT=0 disables it (A/B)
+    static const int cut_env = getenv("RR_KNN_CUT") && getenv("RR_KNN_CUT")[0] == '0' ? 0 : 1;
+    float* const prune = cut_env && dtype != RR_I8 && out_uncertain && k < p.KC ? prune_thr : nullptr;
+    // RR_KNN_FSEL=0: the unstaged final select (A/B)
+    static const int fsel = getenv("RR_KNN_FSEL") ? atoi(getenv("RR_KNN_FSEL")) : 1;
+    const int stage = fsel && p.nchunks <= FSEL_MAXCH;
+    hipLaunchKernelGGL(k_final_select, dim3(nq), dim3(SEL_THREADS), stage ? FSEL_LDS : 0, s, cand_k, cand_i, cnt,
+                       p.nchunks, p.KC, sel_k, sel_i, sel_thr, stage, k, q_f32, d, delta_scale, prune);
+    hipLaunchKernelGGL(k_rescore, dim3((p.npow2 + 3) / 4, nq), dim3(256), 0, s, sel_i, p.KC, p.npow2, db_f32, q_f32, d,
+                       fin_s, fin_i, sel_k, (const float*)prune);
     hipLaunchKernelGGL(k_final_sort, dim3(nq), dim3(SEL_THREADS), fin_lds, s, fin_s, fin_i, p.npow2, k, idx_offset,
                        out_scores, out_idx, sel_thr, q_f32, d, delta_scale, out_uncertain, i8_cert ? i8_qamax : nullptr,
                        i8_qstride, i8_cert ? i8_dbamax : nullptr);

@@ -422,3 +422,31 @@ def test_int8_quantization_and_score_gemm(cuda):
         np.testing.assert_allclose(s[:6].cpu().numpy(), ref_s, rtol=0, atol=1e-12)
         s2, i2 = KnnIndex(db, "bf16").search(qq, 100)
         assert torch.equal(i, i2) and torch.equal(s, s2)
+
+
+@pytest.mark.parametrize("prec", ["fp16", "bf16", "fp32"])
+def test_knn_rescore_cut_changes_nothing(cuda, prec):
+    """The certified re-score cut (rr_knn.hip rescore_cut, on in the checked search):
+    candidates whose screening key is more than twice the error bound below the k-th
+    key are not re-scored; the top-k (indices and float64 scores) equal the uncut
+    search bit for bit, on random rows and on a database with a planted cluster."""
+    from cirtorch import _ops
+    from cirtorch.search import KnnIndex
+    from oracle import data, ops
+    db = _ops.fill_unit_rows(300_000, 512, seed=0xC0FE, device=cuda)
+    q = _ops.fill_unit_rows(200, 512, seed=0xC0FF, device=cuda)
+    index = KnnIndex(db, prec)
+    s0, i0 = index.search(q, 100)                       # unchecked: every candidate re-scored
+    s1, i1, unc = index.search_checked(q, 100)          # checked: the cut
+    assert torch.equal(i0, i1) and torch.equal(s0, s1)
+    assert int(unc.sum()) == 0
+    d = 128
+    qq = data.unit_rows(4, d, seed=62)
+    pl = data.unit_rows(170000, d, seed=64)
+    pl[140000:140600] = qq[2] + 0.3 * data.unit_rows(600, d, seed=65)
+    pl[140000:140600] /= np.linalg.norm(pl[140000:140600], axis=1, keepdims=True)
+    ix = KnnIndex(torch.from_numpy(pl).to(cuda), prec)
+    sv, iv = ix.search(torch.from_numpy(qq).to(cuda), 100, verify=True)
+    ref_s, ref_i = ops.topk_exact(pl, qq, 100)
+    np.testing.assert_array_equal(iv.cpu().numpy(), ref_i)
+    np.testing.assert_allclose(sv.cpu().numpy(), ref_s, rtol=0, atol=1e-12)

@@ -35,19 +35,19 @@ for STEP in "$@"; do
       timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-extras --latency 0 --pcie-steps 0 --local-kpts 0 --fp16-steps 0 --tune "$TUNE" > "$OUT/benchq_$i.json" 2> "$OUT/benchq_$i.err" || { tail -20 "$OUT/benchq_$i.err"; exit 1; }
       python3 -c "
 import json
-d=json.loads(open('$OUT/benchq_$i.json').read().strip().splitlines()[-1]); print('tune=%-12s' % '$TUNE', '%.1f img/s' % d['value'], '%.3f ms' % d['ms_per_step'], 'knn %.3f ms' % d.get('knn', {}).get('ms_per_batch', 0), 'extract %.1f img/s' % d['extract_images_per_sec'], 'body %.3f ms' % d['roofline_layers']['measured_ms'])" ;;
+d=json.loads(open('$OUT/benchq_$i.json').read().strip().splitlines()[-1]); print('tune=%-12s' % '$TUNE', '%.1f img/s' % d['value'], '%.3f ms' % d['ms_per_step'], 'knn %.3f ms' % (d.get('knn') or {}).get('ms_per_batch', 0), 'extract %.1f img/s' % d['extract_images_per_sec'], 'body %.3f ms' % d['roofline_layers']['measured_ms'])" ;;
     benchargs:*)
       BARGS=${STEP#benchargs:}
       timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-extras --latency 0 --pcie-steps 0 --local-kpts 0 --fp16-steps 0 $BARGS > "$OUT/benchargs_$i.json" 2> "$OUT/benchargs_$i.err" || { tail -20 "$OUT/benchargs_$i.err"; exit 1; }
       python3 -c "
 import json
-d=json.loads(open('$OUT/benchargs_$i.json').read().strip().splitlines()[-1]); print('args=%-30s' % '$BARGS', '%.1f img/s' % d['value'], '%.3f ms' % d['ms_per_step'], 'knn %.3f ms' % d.get('knn', {}).get('ms_per_batch', 0), 'extract %.1f img/s' % d['extract_images_per_sec'], 'body %.3f ms' % d['roofline_layers']['measured_ms'])" ;;
+d=json.loads(open('$OUT/benchargs_$i.json').read().strip().splitlines()[-1]); print('args=%-30s' % '$BARGS', '%.1f img/s' % d['value'], '%.3f ms' % d['ms_per_step'], 'knn %.3f ms' % (d.get('knn') or {}).get('ms_per_batch', 0), 'extract %.1f img/s' % d['extract_images_per_sec'], 'body %.3f ms' % d['roofline_layers']['measured_ms'])" ;;
     benchenv:*)
       ENVV=${STEP#benchenv:}
       env $ENVV timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-extras --latency 0 --pcie-steps 0 --local-kpts 0 --fp16-steps 0 > "$OUT/benchenv_$i.json" 2> "$OUT/benchenv_$i.err" || { tail -20 "$OUT/benchenv_$i.err"; exit 1; }
       python3 -c "
 import json
-d=json.loads(open('$OUT/benchenv_$i.json').read().strip().splitlines()[-1]); print('env=%-24s' % '$ENVV', '%.1f img/s' % d['value'], '%.3f ms' % d['ms_per_step'], 'knn %.3f ms' % d.get('knn', {}).get('ms_per_batch', 0), 'extract %.1f img/s' % d['extract_images_per_sec'], 'body %.3f ms' % d['roofline_layers']['measured_ms'])" ;;
+d=json.loads(open('$OUT/benchenv_$i.json').read().strip().splitlines()[-1]); print('env=%-24s' % '$ENVV', '%.1f img/s' % d['value'], '%.3f ms' % d['ms_per_step'], 'knn %.3f ms' % (d.get('knn') or {}).get('ms_per_batch', 0), 'extract %.1f img/s' % d['extract_images_per_sec'], 'body %.3f ms' % d['roofline_layers']['measured_ms'])" ;;
     tests)
       timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
         > "$OUT/pytest_gpu.log" 2>&1 || { tail -30 "$OUT/pytest_gpu.log"; exit 1; }

@@ -16,7 +16,9 @@ def main():
     ap.add_argument("--n", type=int, default=1_000_000)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--tune", default="", help="rr_set_tuning pairs key=value[,key=value]")
-    ap.add_argument("--screen", default="int8", help="screening dtype (int8 / fp16 / bf16 / fp32)")
+    ap.add_argument("--screen", default="fp16", help="screening dtype (int8 / fp16 / bf16 / fp32)")
+    ap.add_argument("--no-verify", dest="verify", action="store_false",
+                    help="unverified search (default: the bench's certified search, certificate resolved)")
     args = ap.parse_args()
     from cirtorch import _ops
     from cirtorch import _engine as E
@@ -27,16 +29,23 @@ def main():
     db = _ops.fill_unit_rows(args.n, 2048, seed=0xDB5EED)
     q = _ops.fill_unit_rows(args.q, 2048, seed=0x0E5EED)
     idx = KnnIndex(db, args.screen)
-    idx.search(q, 100)
+    def one():
+        if args.verify:
+            return idx.search(q, 100, verify="deferred")[2]
+        idx.search(q, 100)
+        return None
+    p = one()
+    if p is not None:
+        p.resolve()
     torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
-    for _ in range(args.reps):
-        idx.search(q, 100)
+    pends = [one() for _ in range(args.reps)]
     b.record()
+    nre = sum(p.resolve() for p in pends if p is not None)
     torch.cuda.synchronize()
-    print("search Q=%d N=%d screen=%s tune=%s: %.3f ms" % (args.q, args.n, args.screen, args.tune,
-                                                          a.elapsed_time(b) / args.reps))
+    print("search Q=%d N=%d screen=%s verify=%s tune=%s: %.3f ms (re-searched %d)"
+          % (args.q, args.n, args.screen, args.verify, args.tune, a.elapsed_time(b) / args.reps, nre))
 
 
 if __name__ == "__main__":

@@ -1,5 +1,5 @@
 """Workload for the HBM-traffic counter passes of the kNN search (the bench's
-match kernels): a 1M x 2048 bf16-screened database, ITERS searches of Q
+match kernels): a 1M x 2048 database (fp16 screening copy by default), ITERS certified searches of Q
 queries (top-100) between two marker kernels, so tools/pmc_parse.py picks
 exactly the searches' dispatches out of the rocprofv3 counter CSV.
 
@@ -37,10 +37,10 @@ def main():
         index.search(q, 100)
     torch.cuda.synchronize()
     _ops.l2n_rows(marker.view(1, 64))          # marker: search dispatches follow
-    for _ in range(args.iters):
-        index.search(q, 100)
+    pends = [index.search(q, 100, verify="deferred")[2] for _ in range(args.iters)]   # the bench's search
     _ops.l2n_rows(marker.view(1, 64))          # marker: end
     torch.cuda.synchronize()
+    assert sum(p.resolve() for p in pends) == 0
     print("done", args.iters, "searches of", args.q, "queries vs", args.n)
 
 

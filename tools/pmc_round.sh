@@ -3,12 +3,12 @@
 # 3 TCC slots, WRITE_SIZE 2 — never together), HBM bytes of the extractor body
 # (128-image forwards) and of the kNN search (Q = 128 and 1024), plus the
 # MFMA busy cycles of the body.
-#   bash tools/pmc_round.sh <outdir> [precision (default fp16)] [kNN screen (default int8)]
+#   bash tools/pmc_round.sh <outdir> [precision (default fp16)] [kNN screen (default fp16)]
 set -e
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT="$ROOT/$1"
 PREC=${2:-fp16}
-SCREEN=${3:-int8}
+SCREEN=${3:-fp16}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 for C in FETCH_SIZE WRITE_SIZE; do
