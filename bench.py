@@ -81,9 +81,9 @@ def parse():
     ap.add_argument("--search-cus", type=int, default=0,
                     help="cap the CUs the step's persistent search kernels spread over (RR_TUNE_GRID_CUS set "
                          "around the search launches only), leaving the rest to the overlapped extraction; 0 = all")
-    ap.add_argument("--cpu-images", type=int, default=12,
+    ap.add_argument("--cpu-images", type=int, default=24,
                     help="images of the CPU baseline's extract sample (batch 1, as scripts/test.py)")
-    ap.add_argument("--cpu-queries", type=int, default=32, help="queries of the CPU baseline's match sample")
+    ap.add_argument("--cpu-queries", type=int, default=64, help="queries of the CPU baseline's match sample")
     ap.add_argument("--cpu-db-rows", type=int, default=1_000_000,
                     help="rows of the CPU baseline's match sample (1M = the full headline DB, no extrapolation)")
     ap.add_argument("--no-extras", dest="extras", action="store_false",
@@ -309,6 +309,16 @@ def kernel_source_digest():
         h.update(os.path.basename(f).encode())
         h.update(open(f, "rb").read())
     return h.hexdigest()[:12]
+
+
+def build_provenance():
+    """which sources the loaded librr.so was built from (rr_build_info) vs the tree it runs in"""
+    from cirtorch import _engine as E
+    info = E.lib().rr_build_info().decode()
+    built = dict(kv.split("=", 1) for kv in info.split())
+    tree = kernel_source_digest()
+    return {"library": os.path.relpath(E.LIB_PATH, REPO), "library_source_digest": built.get("source_digest"),
+            "tree_source_digest": tree, "match": built.get("source_digest") == tree}
 
 
 def pmc_file(kind, match):
@@ -1136,6 +1146,7 @@ def main():
                             "note": "sum over the body's 53 conv layers of max(FLOPs/peak_mfma, algorithmic HBM bytes/"
                                     "peak_hbm) for the step's images, over the measured extractor time"},
         "extract_images_per_sec": ext_only * world,
+        "build": build_provenance(),
         "dist": {"world_size": dist.get_world_size() if dist.is_initialized() else 1,
                  "backend": dist.get_backend() if dist.is_initialized() else None,
                  "note": "backend nccl = RCCL over xGMI on ROCm"},

@@ -36,6 +36,7 @@ class ConvDesc(ctypes.Structure):
 _vp, _i, _ll, _f, _d, _sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_float, ctypes.c_double, ctypes.c_size_t
 _SIGS = {
     "rr_version": ([], _i),
+    "rr_build_info": ([], ctypes.c_char_p),
     "rr_last_error": ([], ctypes.c_char_p),
     "rr_device_arch": ([ctypes.c_char_p, _i], _i),
     "rr_image_to_nhwc": ([_vp, _i, _i, _i, _i, ctypes.POINTER(_f), ctypes.POINTER(_f), _i, _vp, _i, _i, _vp], _i),

@@ -41,6 +41,10 @@ enum rr_layout { RR_NHWC = 0, RR_NCHW = 1 };
 
 /* ------------------------------------------------------------------ runtime */
 int rr_version(void);
+/* "source_digest=<12 hex> arch=gfx950": the sha1 digest of csrc/*.hip, csrc/*.h and this
+ * header the library was built from (tools/src_digest.py), for the provenance of a prebuilt
+ * librr.so. */
+const char* rr_build_info(void);
 const char* rr_last_error(void);
 /* Device architecture name of the current device (e.g. "gfx950"). */
 int rr_device_arch(char* buf, int buflen);

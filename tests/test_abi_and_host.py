@@ -209,3 +209,17 @@ def test_comm_entry_points_validate_arguments():
     assert lib.rr_topk_allgather_workspace_bytes(8, 1024, 100) >= 2 * 8 * 1024 * 100 * 8
     assert lib.rr_topk_allgather_workspace_bytes(0, 1, 1) == 0
     assert lib.rr_topk_allgather_merge(None, None, None, 1, 1, None, None, None, 0, None) != 0
+
+
+def test_library_built_from_this_tree():
+    """rr_build_info: librr.so records the digest of the kernel sources it was built from
+    (tools/src_digest.py, the digest bench.py reports as build.tree_source_digest); the
+    library in the tree must be built from the tree's sources (provenance of a prebuilt
+    librr.so pushed to a GPU box)."""
+    import importlib.util
+    from cirtorch import _engine as E
+    spec = importlib.util.spec_from_file_location("src_digest", os.path.join(REPO, "tools", "src_digest.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    info = E.lib().rr_build_info().decode()
+    assert info == "source_digest=%s arch=gfx950" % m.digest(), info
