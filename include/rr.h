@@ -41,7 +41,7 @@ enum rr_layout { RR_NHWC = 0, RR_NCHW = 1 };
 
 /* ------------------------------------------------------------------ runtime */
 int rr_version(void);
-/* "source_digest=<12 hex> arch=gfx950": the sha1 digest of csrc/*.hip, csrc/*.h and this
+/* "source_digest=<12 hex> arch=gfx950": the sha1 digest of the csrc .hip / .h sources and this
  * header the library was built from (tools/src_digest.py), for the provenance of a prebuilt
  * librr.so. */
 const char* rr_build_info(void);
