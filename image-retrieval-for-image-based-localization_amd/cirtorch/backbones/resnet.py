@@ -215,11 +215,19 @@ class ResNet(nn.Module):
             pair = self._pairable(steps[-1], nxt)
             fuse_proj = pair and proj is not None and self._proj_fusable(proj)
             res = t if proj is None else (None if fuse_proj else self._conv(t, proj))
+            # the whole block (3x3 + boundary pair) in one launch: the 3x3 is not run on its own
+            block = pair and self._c3pairable(t, steps, nxt, fuse_proj)
             y = t
-            for j, st in enumerate(steps[:-1]):
+            for j, st in enumerate(steps[:-2] if block else steps[:-1]):
                 y = pending if (j == 0 and pending is not None) else self._conv(y, st)
             pending = None
-            if pair:
+            if block:
+                mid, last = steps[-2], steps[-1]
+                t, pending = _ops.conv3x3_pair(y, mid.w, mid.scale, mid.shift, mid.leaky, mid.slope,
+                                               last.w, last.scale, last.shift, res, last.leaky, last.slope,
+                                               nxt.w, nxt.scale, nxt.shift, nxt.c_out, nxt.leaky, nxt.slope,
+                                               proj=(t, proj.w, proj.scale, proj.shift) if fuse_proj else None)
+            elif pair:
                 last = steps[-1]
                 t, pending = _ops.conv1x1_pair(y, last.w, last.scale, last.shift, res, last.leaky, last.slope,
                                                nxt.w, nxt.scale, nxt.shift, nxt.c_out, nxt.leaky, nxt.slope,
@@ -250,6 +258,20 @@ class ResNet(nn.Module):
         """stride-1 1x1 projection 64 -> 256 (first block of the 256-channel stage), identity activation"""
         return (proj.kh == 1 and proj.stride == 1 and proj.pad == 0 and proj.perm and proj.c_out == 256
                 and proj.w.shape[1] == 64 and not proj.leaky)
+
+    @staticmethod
+    def _c3pairable(t, steps, nxt, fuse_proj):
+        """a 256-channel-stage bottleneck (1x1 -> 3x3 64 -> 64 -> 1x1 64 -> 256) whose boundary pairs
+        with the next block's conv1: rr_conv3x3_pair runs the 3x3 and the pair as one launch
+        (t2 never reaches HBM).  Needs H % 4 == 0 and W % 32 == 0; RR_C3PAIR=0 keeps two launches."""
+        if len(steps) != 3 or os.environ.get("RR_C3PAIR", "1") == "0":
+            return False
+        mid, last = steps[1], steps[2]
+        n, h, w, c = t.shape
+        return (mid.kh == 3 and mid.kw == 3 and mid.stride == 1 and mid.pad == 1 and mid.perm and mid.c_out == 64
+                and tuple(mid.w.shape) == (64, 576) and last.c_out == 256 and last.w.shape[1] == 64
+                and nxt.c_out in ((64,) if fuse_proj else (64, 128)) and h % 4 == 0 and w % 32 == 0
+                and n * h * w * 64 * 2 < 2 ** 31)
 
     def _pairable(self, last, nxt):
         """conv3 of a bottleneck followed by a stride-1 1x1 conv1 of the next block: one fused

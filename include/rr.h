@@ -113,6 +113,23 @@ int rr_conv1x1_pair(const void* x, long long p, int c_in, const void* w3, const 
                     const float* scale1, const float* shift1, int c_out, int act1, float slope1, void* y,
                     void* z, int dtype, void* stream);
 
+/* One bottleneck block of the 256-channel stage fused (bf16 or fp16 dtype, PERM32 weights):
+ *   t2 = act2(conv3x3(t1, w33) * scale2 + shift2)                 3x3 / s1 / p1, 64 -> 64
+ *   y  = act3(conv1x1(t2, w3) * scale3 + shift3 + shortcut)       64 -> 256
+ *   z  = act1(conv1x1(y, w1) * scale1 + shift1)                   256 -> c_out (64 or 128)
+ * conv2 .. conv3 + residual of ResidualBlock i and conv1 of block i + 1
+ * (cirtorch/backbones/misc.py:163-203) in one pass: t2 never reaches HBM and the 3x3's
+ * matrix work runs beside the boundary's memory traffic.  shortcut = residual ([p][256]) or,
+ * with residual == NULL, the projection proj_bn(proj_conv(xp)) (c_out 64).  t1 [n][h][w][64],
+ * h % 4 == 0, w % 32 == 0; y / z bit-identical to the unfused launches (the 3x3 kernel +
+ * rr_conv1x1_pair).  RR_EINVAL for other shapes (the caller runs those launches instead). */
+int rr_conv3x3_pair(const void* t1, int n, int h, int w, const void* w33, const float* scale2,
+                    const float* shift2, int act2, float slope2, const void* w3, const float* scale3,
+                    const float* shift3, const void* residual, const void* xp, const void* wp,
+                    const float* scalep, const float* shiftp, int act3, float slope3, const void* w1,
+                    const float* scale1, const float* shift1, int c_out, int act1, float slope1, void* y,
+                    void* z, int dtype, void* stream);
+
 /* 3x3/s2/p1 style max pooling, NHWC.  Replaces nn.MaxPool2d(3, stride=2,
  * padding=1) of the stem (cirtorch/backbones/resnet.py:65). */
 int rr_maxpool2d(const void* x, int n, int h, int w, int c, int k, int stride, int pad,
