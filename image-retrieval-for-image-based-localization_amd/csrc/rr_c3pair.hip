@@ -57,7 +57,8 @@ __device__ __forceinline__ ci32x4_t crsrc(const void* base, unsigned bytes) {
     return r;
 }
 
-__device__ __forceinline__ void cbar() { asm volatile("s_barrier" ::: "memory"); }
+// t2 reaches the LDS by ds_write (not DMA): its writes must be done before the barrier
+__device__ __forceinline__ void cbar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // k_stream_pair's weight image swizzle (every ds_read_b128 lane group of an A fragment hits
 // 16 distinct 4-bank groups)
