@@ -1411,43 +1411,73 @@ __global__ void __launch_bounds__(512, 1) k_gemm8a(ConvArgs a, int tiles_p, int 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int grp = wave >> 2, wn = wave & 3;
-    const int bx = (int)blockIdx.x, xcd = bx & 7;
+    // persistent blocks over an XCD-contiguous tile range (k_gemm8's walk): XCD x owns
+    // [s_x, s_x + n_x), its nb_x blocks stride through it; grid = ntiles is one tile per block
+    const int nwg = (int)gridDim.x, bx = (int)blockIdx.x, xcd = bx & 7;
     const int nt8 = ntiles >> 3, rt8 = ntiles & 7;
-    const int t = (xcd < rt8 ? xcd * (nt8 + 1) : rt8 * (nt8 + 1) + (xcd - rt8) * nt8) + (bx >> 3);
-    if (t >= ntiles) return;
+    const int s_x = xcd < rt8 ? xcd * (nt8 + 1) : rt8 * (nt8 + 1) + (xcd - rt8) * nt8;
+    const int n_x = nt8 + (xcd < rt8 ? 1 : 0);
+    const int nb_x = (nwg >> 3) + (xcd < (nwg & 7) ? 1 : 0);
+    int li = bx >> 3;
+    if (li >= n_x) return;
     const int H = a.h, W = a.w_, Cin = a.cin;
     const unsigned tap_magic = tapu_magic(a.kh * a.kw);  // tapu_k0
     const int nk = a.kp / 64;
     const unsigned lds0 = (unsigned)(unsigned long long)smem;
     const int lrow = lane >> 3, lchunk = (lane & 7) ^ (lrow & 7);
+    const int r16 = lane & 15, kq = lane >> 4;
 
-    const int c0 = (t / tiles_p) * 128, p0 = (t % tiles_p) * 256;
-    const long long arows = min(128, a.cout - c0);
-    const i32x4_t rsA = make_rsrc((const char*)a.w + (long long)c0 * a.kp * ESZ, (unsigned)(arows * a.kp * ESZ));
+    // c_out = 128 (gemm8a_eligible): one channel tile, so this lane's 2 x 8 BN scale / shift
+    // stay in registers for every tile (the epilogue issues no global load: a load there
+    // would wait, vmcnt being in order, for the next tile's prologue DMA)
+    const bool affine = a.flags & RR_CONV_AFFINE;
+    float esc[2][8], esh[2][8];
+#pragma unroll
+    for (int i2 = 0; i2 < 2; ++i2) {
+        const int c = grp * 64 + 32 * i2 + 8 * kq;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            esc[i2][r] = affine ? a.scale[c + r] : 1.f;
+            esh[i2][r] = affine ? a.shift[c + r] : 0.f;
+        }
+    }
+#pragma unroll
+    for (int i2 = 0; i2 < 2; ++i2)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(esc[i2][r]), "+v"(esh[i2][r]));
+
+    int p0 = 0;
+    const i32x4_t rsA = make_rsrc((const char*)a.w, (unsigned)(128ll * a.kp * ESZ));
     const i32x4_t rsB = make_rsrc(a.x, (unsigned)((long long)a.n * H * W * Cin * ESZ));
     unsigned a_off[2], b_base[2][2];
     int b_hi[2][2], b_wi[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int arow = (wave + 8 * i) * 8 + lrow;
-        a_off[i] = arow < arows ? (unsigned)(((long long)arow * a.kp + lchunk * VEC) * ESZ) : OOB;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int p = p0 + h * 128 + (wave + 8 * i) * 8 + lrow;
-            if (p < a.P) {
-                const int img = p / (a.ho * a.wo);
-                const int rem = p - img * (a.ho * a.wo);
-                const int oh = rem / a.wo, ow = rem - oh * a.wo;
-                b_hi[h][i] = oh * a.stride - a.pad;
-                b_wi[h][i] = ow * a.stride - a.pad;
-                b_base[h][i] = (unsigned)((long long)img * H * W * Cin +
-                                          ((long long)b_hi[h][i] * W + b_wi[h][i]) * Cin + lchunk * VEC);
-            } else {
-                b_hi[h][i] = b_wi[h][i] = -(1 << 28);
-                b_base[h][i] = OOB;
-            }
-        }
+        a_off[i] = (unsigned)(((long long)arow * a.kp + lchunk * VEC) * ESZ);
     }
+    auto setup = [&](int t) {
+        p0 = t * 256;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int p = p0 + h * 128 + (wave + 8 * i) * 8 + lrow;
+                if (p < a.P) {
+                    const int img = p / (a.ho * a.wo);
+                    const int rem = p - img * (a.ho * a.wo);
+                    const int oh = rem / a.wo, ow = rem - oh * a.wo;
+                    b_hi[h][i] = oh * a.stride - a.pad;
+                    b_wi[h][i] = ow * a.stride - a.pad;
+                    b_base[h][i] = (unsigned)((long long)img * H * W * Cin +
+                                              ((long long)b_hi[h][i] * W + b_wi[h][i]) * Cin + lchunk * VEC);
+                } else {
+                    b_hi[h][i] = b_wi[h][i] = -(1 << 28);
+                    b_base[h][i] = OOB;
+                }
+            }
+    };
+    setup(s_x + li);
     // K-step descriptor, once per K-step (k_gemm8's KD: no division on the issue path)
     const unsigned kw_magic = tapu_magic(a.kw);
     struct KD {
@@ -1475,7 +1505,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm8a(ConvArgs a, int tiles_p, int 
         if (X == 0) {
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                const unsigned off = (d.live && a_off[i] != OOB) ? a_off[i] + (unsigned)(d.k0 * 2) : OOB;
+                const unsigned off = d.live ? a_off[i] + (unsigned)(d.k0 * 2) : OOB;
                 dma16(rsA, off, dst + (wave + 8 * i) * 1024);
             }
         } else {
@@ -1504,7 +1534,6 @@ __global__ void __launch_bounds__(512, 1) k_gemm8a(ConvArgs a, int tiles_p, int 
         for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int j = 0; j < 2; ++j) acc[qb][i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-    const int r16 = lane & 15, kq = lane >> 4;
     uint4 fa[4][2], fb[2][2];
     auto read_a = [&](int kt) {
         const char* base = smem + (kt % 3) * ST;
@@ -1544,83 +1573,100 @@ __global__ void __launch_bounds__(512, 1) k_gemm8a(ConvArgs a, int tiles_p, int 
         __builtin_amdgcn_sched_barrier(0);
     };
     auto bar = []() { asm volatile("s_barrier" ::: "memory"); };
-
-    {
+    auto prologue = [&]() {
         const KD d0 = kdesc(0), d1 = kdesc(1);
         issue(0, d0); issue(1, d0); issue(2, d0);
         issue(0, d1); issue(1, d1); issue(2, d1);
-    }
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // K-step 0's A0 / B0
-    bar();
-    if (grp == 1) bar();
-    for (int kt = 0; kt < nk; ++kt) {
-        const KD d2 = kdesc(kt + 2);
-        // phase A: A0 x B0 of K-step kt; K-step kt + 2's A0 / B0
-        read_a(kt); read_b(kt, 0);
-        issue(0, d2); issue(1, d2);
-        asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // K-step kt's B1 has landed
-        bar(); mfma_q(0); bar();
-        // phase B: A0 (registers) x B1; K-step kt + 2's B1
-        read_b(kt, 1);
-        issue(2, d2);
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // K-step kt + 1's A0 / B0 have landed
-        bar(); mfma_q(1); bar();
-    }
-    if (grp == 0) bar();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
 
-    // ---- epilogue (PERM32 rows): folded BN scale / shift, residual, activation, NHWC store
     T* __restrict__ Y = (T*)a.y;
     const T* __restrict__ R = (const T*)a.res;
-    const bool affine = a.flags & RR_CONV_AFFINE;
     const bool resid = a.flags & RR_CONV_RESIDUAL;
     const bool leaky = a.act == RR_ACT_LEAKY;
-#pragma unroll
-    for (int i2 = 0; i2 < 2; ++i2) {
-        const int c = c0 + grp * 64 + 32 * i2 + 8 * kq;  // 8 consecutive channels
-        if (c >= a.cout) continue;
-        float sc[8], sh[8];
-        if (affine) {
-            St4<float>::ld(a.scale + c, sc);
-            St4<float>::ld(a.scale + c + 4, sc + 4);
-            St4<float>::ld(a.shift + c, sh);
-            St4<float>::ld(a.shift + c + 4, sh + 4);
-        } else {
-#pragma unroll
-            for (int r = 0; r < 8; ++r) { sc[r] = 1.f; sh[r] = 0.f; }
+    prologue();
+    // the previous tile's epilogue issued exactly ST_FULL stores and nothing else (a full
+    // tile, no residual load); they are younger than this tile's prologue
+    constexpr int ST_FULL = 8;
+    bool prev_full = false;
+    for (;;) {
+        // K-step 0's A0 / B0 have landed: younger are its B1, K-step 1 (8) and the
+        // previous tile's epilogue stores; an epilogue with loads / fewer stores is
+        // waited for with it
+        if (prev_full) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // 8 + ST_FULL
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        static_assert(8 + ST_FULL == 16, "the counted wait above");
+        bar();
+        if (grp == 1) bar();
+        for (int kt = 0; kt < nk; ++kt) {
+            const KD d2 = kdesc(kt + 2);
+            // phase A: A0 x B0 of K-step kt; K-step kt + 2's A0 / B0
+            read_a(kt); read_b(kt, 0);
+            issue(0, d2); issue(1, d2);
+            asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // K-step kt's B1 has landed
+            bar(); mfma_q(0); bar();
+            // phase B: A0 (registers) x B1; K-step kt + 2's B1
+            read_b(kt, 1);
+            issue(2, d2);
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // K-step kt + 1's A0 / B0 have landed
+            bar(); mfma_q(1); bar();
         }
+        if (grp == 0) bar();  // equal barrier counts: every wave's LDS reads of this tile are done
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing (zero) K-step DMAs have landed
+
+        // the next tile's prologue DMA flies while this tile's epilogue runs
+        const int ep0 = p0;
+        li += nb_x;
+        const bool more = li < n_x;
+        if (more) {
+            setup(s_x + li);
+            prologue();
+        }
+        prev_full = !resid && ep0 + 256 <= a.P;
+        // ---- epilogue (PERM32 rows): folded BN scale / shift, residual, activation, NHWC store
+#pragma unroll
+        for (int i2 = 0; i2 < 2; ++i2) {
+            const int c = grp * 64 + 32 * i2 + 8 * kq;  // 8 consecutive channels
+#pragma unroll
+            for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int p = ep0 + qb * 128 + wn * 32 + j * 16 + r16;
+                    if (p >= a.P) continue;
+                    float v[8];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        v[r] = acc[qb][2 * i2][j][r] * esc[i2][r] + esh[i2][r];
+                        v[4 + r] = acc[qb][2 * i2 + 1][j][r] * esc[i2][4 + r] + esh[i2][4 + r];
+                    }
+                    const long long o = (long long)p * a.ldy + c;
+                    if (resid) {
+                        float rv[8];
+                        St4<T>::ld(R + o, rv);
+                        St4<T>::ld(R + o + 4, rv + 4);
+#pragma unroll
+                        for (int r = 0; r < 8; ++r) v[r] += rv[r];
+                    }
+                    if (leaky) {
+#pragma unroll
+                        for (int r = 0; r < 8; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * a.slope;
+                    }
+                    uint4 q;
+                    q.x = H16<T>::pack2(v[0], v[1]);
+                    q.y = H16<T>::pack2(v[2], v[3]);
+                    q.z = H16<T>::pack2(v[4], v[5]);
+                    q.w = H16<T>::pack2(v[6], v[7]);
+                    *reinterpret_cast<uint4*>(Y + o) = q;
+                }
+        }
+        if (!more) break;
 #pragma unroll
         for (int qb = 0; qb < 2; ++qb)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int p = p0 + qb * 128 + wn * 32 + j * 16 + r16;
-                if (p >= a.P) continue;
-                float v[8];
+            for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    v[r] = acc[qb][2 * i2][j][r] * sc[r] + sh[r];
-                    v[4 + r] = acc[qb][2 * i2 + 1][j][r] * sc[4 + r] + sh[4 + r];
-                }
-                const long long o = (long long)p * a.ldy + c;
-                if (resid) {
-                    float rv[8];
-                    St4<T>::ld(R + o, rv);
-                    St4<T>::ld(R + o + 4, rv + 4);
-#pragma unroll
-                    for (int r = 0; r < 8; ++r) v[r] += rv[r];
-                }
-                if (leaky) {
-#pragma unroll
-                    for (int r = 0; r < 8; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * a.slope;
-                }
-                uint4 q;
-                q.x = H16<T>::pack2(v[0], v[1]);
-                q.y = H16<T>::pack2(v[2], v[3]);
-                q.z = H16<T>::pack2(v[4], v[5]);
-                q.w = H16<T>::pack2(v[6], v[7]);
-                *reinterpret_cast<uint4*>(Y + o) = q;
-            }
+                for (int j = 0; j < 2; ++j) acc[qb][i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 static int g_gemm8 = -1;  // rr_set_tuning(RR_TUNE_GEMM8) / RR_GEMM8: 0 off, 1 auto (default), 2 force where legal
@@ -1731,6 +1777,7 @@ static bool try_gemm8h(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
 }
 
 static int g_gemm8a = 1;  // rr_set_tuning(RR_TUNE_GEMM8, value | 16): k_gemm8a off
+static bool g_gemm8a_tile = false;  // RR_TUNE_GEMM8 value | 128: k_gemm8a one block per tile
 
 // k_gemm8a: 16-bit PERM32 convs with 128-multiple c_out below 256 (1x1 or
 // tap-uniform im2col), enough 128 x 256 tiles to fill the chip twice.
@@ -1750,9 +1797,11 @@ static bool try_gemm8a(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
     } else {
         if (!perm || !gemm8a_eligible(a, k1)) return false;
         const int tiles_p = (a.P + 255) / 256;
-        const int ntiles = tiles_p * (a.cout / 128);
-        if (k1) hipLaunchKernelGGL((k_gemm8a<T, 1>), dim3(ntiles), dim3(512), 0, s, a, tiles_p, ntiles);
-        else hipLaunchKernelGGL((k_gemm8a<T, 2>), dim3(ntiles), dim3(512), 0, s, a, tiles_p, ntiles);
+        const int ntiles = tiles_p;  // c_out = 128: one channel tile
+        // persistent (RR_TUNE_GEMM8 value | 128: one block per tile)
+        const int grid = g_gemm8a_tile ? ntiles : std::min(ntiles, grid_cus());
+        if (k1) hipLaunchKernelGGL((k_gemm8a<T, 1>), dim3(grid), dim3(512), 0, s, a, tiles_p, ntiles);
+        else hipLaunchKernelGGL((k_gemm8a<T, 2>), dim3(grid), dim3(512), 0, s, a, tiles_p, ntiles);
         return true;
     }
 }
@@ -1849,6 +1898,7 @@ void set_gemm_tuning(int key, int value) {
         g_gemm8s = !(value >= 0 && (value & 32));
         g_gemm8_tile = value >= 0 && (value & 4);
         g_gemm8_pmajor = !(value >= 0 && (value & 64));
+        g_gemm8a_tile = value >= 0 && (value & 128);
         value = value < 0 ? 0 : value & 3;
         g_gemm8 = value > 2 ? 2 : value;
     }

@@ -359,7 +359,8 @@ int rr_rank_full(const float* db_f32, long long n, const float* q_f32, int nq, i
  *                        persistent everywhere; | 4: one block per tile everywhere; | 8: no
  *                        k_gemm8h / k_gemm8s; | 16: no k_gemm8a; | 32: k_gemm8h instead of the streaming
  *                        k_gemm8s for the <= 128-query score GEMM; | 64: conv tiles walked
- *                        channel-major instead of pixel-major)
+ *                        channel-major instead of pixel-major; | 128: k_gemm8a one block per
+ *                        tile instead of persistent blocks)
  *   RR_TUNE_KNN_FUSED    0/1 kNN screening in the score-GEMM epilogue after a 4-chunk
  *                        prefix (default 1); 0 = every chunk through the score slab
  *   RR_TUNE_CONV3_PIPE   1 (default): the direct 3x3 kernel reads the operands of its next

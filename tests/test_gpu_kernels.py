@@ -803,6 +803,8 @@ def test_gemm8a_bit_identical_to_tiled_engine(cuda, shape, prec):
     E.check(E.lib().rr_set_tuning(5, 0), "rr_set_tuning")
     try:
         a = _ops().conv2d_fused(x, wp, k, k, s, 1, cout, sc, sh, leaky=True, perm32=True)
+        E.check(E.lib().rr_set_tuning(8, 1 | 128), "rr_set_tuning")  # one block per tile
+        c = _ops().conv2d_fused(x, wp, k, k, s, 1, cout, sc, sh, leaky=True, perm32=True)
         E.check(E.lib().rr_set_tuning(8, 1 | 16), "rr_set_tuning")
         b = _ops().conv2d_fused(x, wp, k, k, s, 1, cout, sc, sh, leaky=True, perm32=True)
     finally:
@@ -810,6 +812,7 @@ def test_gemm8a_bit_identical_to_tiled_engine(cuda, shape, prec):
         E.lib().rr_set_tuning(6, 1)
         E.lib().rr_set_tuning(5, 1)
     assert torch.equal(a, b)
+    assert torch.equal(a, c)
     ref = F.conv2d(x[:1].cpu().permute(0, 3, 1, 2).double(), wt.to(dt).cpu().double(), stride=s, padding=1)
     ref = ref * sc.cpu().double()[None, :, None, None] + sh.cpu().double()[None, :, None, None]
     ref = F.leaky_relu(ref, 0.01).permute(0, 2, 3, 1)
