@@ -252,8 +252,7 @@ __global__ void __launch_bounds__(512, 1) k_c3pair(C3PairArgs a, int tiles_w, in
     // ================================================================= pair role state
     const int pw = wave - 4;
     const bool leaky3 = a.act3 == RR_ACT_LEAKY, leaky1 = a.act1 == RR_ACT_LEAKY;
-    constexpr int NRQ = PROJ ? NK3 : NR3;
-    uint4 rq[2][NRQ];  // shortcut (or projection input) fragments of the strip of phase A / B
+    constexpr int NRQ = PROJ ? NK3 : NR3;  // shortcut (or projection input) fragments of a strip
     auto strip_pixel = [&](int t, int k) __attribute__((always_inline)) {  // global pixel of lane r16 in local strip k of tile t
         int img, oh0, ow0;
         tile_org(t, img, oh0, ow0);
@@ -410,20 +409,38 @@ __global__ void __launch_bounds__(512, 1) k_c3pair(C3PairArgs a, int tiles_w, in
             cbar();
         }
     } else {
-        load_rq(rq[0], strip_pixel(tile_id(0), pw));  // step 0's phase-A shortcut
+        // the HBM stream issues ahead of the 3x3 role's MFMA run on the same SIMD
+        // (measured: setprio 1 -2 % per block vs none; 2 the same as 1)
+        __builtin_amdgcn_s_setprio(1);
+        // shortcut fragments two phases ahead (4 buffers: phases A / B of two tiles), so a
+        // pair wave keeps ~16 KiB of loads in flight across the barriers
+        uint4 rq[4][NRQ];
+        load_rq(rq[0], strip_pixel(tile_id(0), pw));
+        load_rq(rq[1], strip_pixel(tile_id(0), 4 + pw));
         cbar();
         cbar();
         cbar();
-        for (int s = 0; s < nmine; ++s) {
-            const int t = tile_id(s);
-            // phase A: strip pw of tile s (t2 strips 0-3), phase B's shortcut prefetched
-            load_rq(rq[1], strip_pixel(t, 4 + pw));
-            pair_strip(pw, strip_pixel(t, pw), rq[0]);
-            cbar();
-            // phase B: strip 4 + pw of tile s, next phase A's shortcut prefetched
-            if (s + 1 < nmine) load_rq(rq[0], strip_pixel(tile_id(s + 1), pw));
-            pair_strip(4 + pw, strip_pixel(t, 4 + pw), rq[1]);
-            cbar();
+        for (int s = 0; s < nmine; s += 2) {
+            {  // tile s from buffers 0 / 1, tile s + 1's into 2 / 3
+                const int t = tile_id(s);
+                const bool n1 = s + 1 < nmine;
+                if (n1) load_rq(rq[2], strip_pixel(tile_id(s + 1), pw));
+                pair_strip(pw, strip_pixel(t, pw), rq[0]);
+                cbar();
+                if (n1) load_rq(rq[3], strip_pixel(tile_id(s + 1), 4 + pw));
+                pair_strip(4 + pw, strip_pixel(t, 4 + pw), rq[1]);
+                cbar();
+            }
+            if (s + 1 < nmine) {  // tile s + 1 from buffers 2 / 3, tile s + 2's into 0 / 1
+                const int t = tile_id(s + 1);
+                const bool n2 = s + 2 < nmine;
+                if (n2) load_rq(rq[0], strip_pixel(tile_id(s + 2), pw));
+                pair_strip(pw, strip_pixel(t, pw), rq[2]);
+                cbar();
+                if (n2) load_rq(rq[1], strip_pixel(tile_id(s + 2), 4 + pw));
+                pair_strip(4 + pw, strip_pixel(t, 4 + pw), rq[3]);
+                cbar();
+            }
         }
     }
 }
