@@ -12,7 +12,7 @@ import csv
 import json
 
 BODY = ("k_stem_pool", "k_conv3x3", "k_stream1x1", "k_stream_pair", "k_igemm", "k_gemm8", "k_pair_mid", "k_gemm8a",
-        "k_c3s_w", "k_wres1x1", "k_c3w64")
+        "k_c3s_w", "k_wres1x1", "k_c3w64", "k_c3pair")
 
 
 def is_body(name, dtype):
