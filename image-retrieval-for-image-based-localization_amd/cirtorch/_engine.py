@@ -44,7 +44,7 @@ _SIGS = {
     "rr_conv1x1_pair": ([_vp, _ll, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _i, _f, _vp, _vp, _vp, _i, _i, _f,
                          _vp, _vp, _i, _vp], _i),
     "rr_conv3x3_pair": ([_vp, _i, _i, _i, _vp, _vp, _vp, _i, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _f,
-                         _vp, _vp, _vp, _i, _i, _f, _vp, _vp, _i, _vp], _i),
+                         _vp, _vp, _vp, _i, _i, _f, _vp, _vp, _vp, _i, _vp], _i),
     "rr_pack_conv_weights": ([_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _vp], _i),
     "rr_stem_pack_weights": ([_vp, _i, _i, _i, _i, _vp, _i, _vp], _i),
     "rr_stem_conv_pool": ([_vp, _i, _i, _i, ctypes.POINTER(_f), ctypes.POINTER(_f), _i, _vp, _vp, _vp, _i, _f, _vp,

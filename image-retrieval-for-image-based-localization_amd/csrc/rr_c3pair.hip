@@ -86,6 +86,7 @@ struct C3PairArgs {
     const float *s1, *h1;
     bf16_t* y;                 // [P][256]
     bf16_t* z;                 // [P][C1]
+    int* queue;                // 8 zeroed per-XCD tile counters (dynamic walk) or NULL (static)
     int n, h, w;
     int act2, act3, act1;
     float slope2, slope3, slope1;
@@ -108,6 +109,7 @@ __global__ void __launch_bounds__(512, 1) k_c3pair(C3PairArgs a, int tiles_w, in
     __shared__ __attribute__((aligned(16))) char sWp[PROJ ? C3 * K3 * 2 : 16];
     __shared__ __attribute__((aligned(16))) float sS3[C3], sH3[C3], sS1[C1], sH1[C1], sS2[64], sH2[64];
     __shared__ __attribute__((aligned(16))) float sSp[PROJ ? C3 : 4], sHp[PROJ ? C3 : 4];
+    __shared__ int sTile[4];  // tile of step s in slot s & 3 (-1: none), fetched three steps ahead
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -142,14 +144,33 @@ __global__ void __launch_bounds__(512, 1) k_c3pair(C3PairArgs a, int tiles_w, in
         sH2[tid] = a.h33[tid];
     }
     const int wc = wave & 1, wpx = (wave >> 1) & 1;  // 3x3 role: channel half, pixel half
-    __syncthreads();
 
-    // ---- this block's tiles: XCD-contiguous walk (k_c3w64's)
-    const int b = (int)blockIdx.x, G = (int)gridDim.x;
-    auto tile_id = [&](int i) __attribute__((always_inline)) { return i * G + (b & 7) * (G >> 3) + (b >> 3); };
-    const int first = (b & 7) * (G >> 3) + (b >> 3);
-    const int nmine = first < ntiles ? (ntiles - 1 - first) / G + 1 : 0;
-    if (nmine == 0) return;  // block-uniform
+    // ---- this block's tiles.  Static: k_c3w64's XCD-contiguous walk.  Dynamic (a.queue):
+    // XCD x = blockIdx & 7 owns the contiguous tile range [s_x, s_x + n_x) and its blocks take
+    // the next tile from the XCD's counter, so a block that starts late (its CU still held by
+    // another stream's kernel) takes fewer tiles instead of finishing its fixed share late.
+    // Thread 0 fetches step s's tile during step s - 3 into sTile (both roles read it after
+    // the barriers that follow).
+    const int b = (int)blockIdx.x, G = (int)gridDim.x, xcd = b & 7;
+    const int nt8 = ntiles >> 3, rt8 = ntiles & 7;
+    const int s_x = xcd < rt8 ? xcd * (nt8 + 1) : rt8 * (nt8 + 1) + (xcd - rt8) * nt8;
+    const int n_x = nt8 + (xcd < rt8 ? 1 : 0);
+    auto fetch_tile = [&](int i) __attribute__((always_inline)) {
+        if (a.queue) {
+            const int v = atomicAdd(a.queue + xcd, 1);
+            return v < n_x ? s_x + v : -1;
+        }
+        const int t = i * G + xcd * (G >> 3) + (b >> 3);
+        return t < ntiles ? t : -1;
+    };
+    if (tid == 0) {
+        sTile[0] = fetch_tile(0);
+        sTile[1] = fetch_tile(1);
+        sTile[2] = fetch_tile(2);
+    }
+    __syncthreads();
+    auto tile_id = [&](int i) __attribute__((always_inline)) { return sTile[i & 3]; };
+    if (tile_id(0) < 0) return;  // block-uniform
     auto tile_org = [&](int t, int& img, int& oh0, int& ow0) __attribute__((always_inline)) {
         img = t / tiles_hw;
         const int rem = t - img * tiles_hw, th = rem / tiles_w;
@@ -164,32 +185,31 @@ __global__ void __launch_bounds__(512, 1) k_c3pair(C3PairArgs a, int tiles_w, in
     auto patch_dma = [&](int t, bool live) __attribute__((always_inline)) {
         int img = 0, oh0 = 0, ow0 = 0;
         if (live) tile_org(t, img, oh0, ow0);
+        // the pieces' per-lane slot values derived per call from an opaque copy of the lane's
+        // row: hoisted out of the tile walk they were spilled, and each reload's vmcnt(0)
+        // serialised the DMA pieces behind it
+        int lr = lrow;
+        asm volatile("" : "+v"(lr));
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            const int d = wave + 4 * u, q = d * 8 + lrow;
+            const int d = wave + 4 * u, q = d * 8 + lr;
             if (d >= NP) break;  // wave-uniform
             const int pr = q / PITCH, pc = q - pr * PITCH;
             const int hh = oh0 - 1 + pr, ww = ow0 - 1 + pc;
             unsigned off = COOB;
             if (live && pc < PCW && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W)
-                off = (unsigned)(((((long long)img * H + hh) * W + ww) * 64 + ((lch ^ lrow) << 3)) * 2);
+                off = (unsigned)(((((long long)img * H + hh) * W + ww) * 64 + ((lch ^ lr) << 3)) * 2);
             cdma16(rsX, off, ldsP + d * 1024);
         }
     };
-    int rel[FN][3][2];  // fragment address bases: pixel fragment j, tap column dx, half-step hs
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-        const int p = wpx * (TP / 2) + j * 16;
-#pragma unroll
-        for (int dx = 0; dx < 3; ++dx) {
-            const int q = (p / TW) * PITCH + (p % TW) + r16 + dx;
-#pragma unroll
-            for (int hs = 0; hs < 2; ++hs) rel[j][dx][hs] = q * 128 + (((kq + 4 * hs) ^ (q & 7)) << 4);
-        }
-    }
     h16_f32x4_t acc[2][FN];
     // the tile's 3x3 (k_c3w64's K-step loop: 18 x (4 fragment reads, 8 MFMAs))
     auto conv3x3 = [&](const uint4 (&areg)[2][18]) __attribute__((always_inline)) {
+        // fragment address bases (pixel fragment j, tap column dx, half-step hs), derived per
+        // tile from an opaque copy of the lane's column: live only across this loop (24 VGPRs),
+        // not across the whole tile walk beside the 144 weight VGPRs
+        int lc = r16;
+        asm volatile("" : "+v"(lc));
         const char* base[FN][3][2];
 #pragma unroll
         for (int j = 0; j < FN; ++j)
@@ -197,9 +217,8 @@ __global__ void __launch_bounds__(512, 1) k_c3pair(C3PairArgs a, int tiles_w, in
             for (int dx = 0; dx < 3; ++dx)
 #pragma unroll
                 for (int hs = 0; hs < 2; ++hs) {
-                    int r = rel[j][dx][hs];
-                    asm volatile("" : "+v"(r));  // per-tile opaque copy: bases stay 24 VGPRs
-                    base[j][dx][hs] = sPatch + r;
+                    const int q = (wpx * 2 + (j >> 1)) * PITCH + (j & 1) * 16 + lc + dx;  // tile pixel wpx*64 + j*16
+                    base[j][dx][hs] = sPatch + q * 128 + (((kq + 4 * hs) ^ (q & 7)) << 4);
                 }
 #pragma unroll
         for (int ii = 0; ii < 2; ++ii)
@@ -391,11 +410,11 @@ __global__ void __launch_bounds__(512, 1) k_c3pair(C3PairArgs a, int tiles_w, in
         conv();
         if (wpx == 0) store_t2();
         cbar();  // every 3x3 wave is done with patch 0
-        patch_dma(tile_id(1), nmine > 1);
+        patch_dma(tile_id(1), tile_id(1) >= 0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         cbar();
-        for (int s = 0; s < nmine; ++s) {
-            const bool more = s + 1 < nmine;
+        for (int s = 0; tile_id(s) >= 0; ++s) {
+            const bool more = tile_id(s + 1) >= 0;
             // phase A: tile s's strips 4-7 (lower pixel half), then tile s + 1's 3x3
             if (wpx == 1) store_t2();
             if (more) conv();
@@ -403,7 +422,10 @@ __global__ void __launch_bounds__(512, 1) k_c3pair(C3PairArgs a, int tiles_w, in
             // phase B: tile s + 1's strips 0-3 (upper pixel half), tile s + 2's patch
             if (more) {
                 if (wpx == 0) store_t2();
-                patch_dma(tile_id(s + 2), s + 2 < nmine);
+                const int t2i = tile_id(s + 2);
+                patch_dma(t2i, t2i >= 0);
+                // step s + 3's tile into the slot step s - 1 used (read by no one after step s - 1)
+                if (tid == 0) sTile[(s + 3) & 3] = t2i >= 0 ? fetch_tile(s + 3) : -1;
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
             cbar();
@@ -420,10 +442,10 @@ __global__ void __launch_bounds__(512, 1) k_c3pair(C3PairArgs a, int tiles_w, in
         cbar();
         cbar();
         cbar();
-        for (int s = 0; s < nmine; s += 2) {
+        for (int s = 0; tile_id(s) >= 0; s += 2) {
             {  // tile s from buffers 0 / 1, tile s + 1's into 2 / 3
                 const int t = tile_id(s);
-                const bool n1 = s + 1 < nmine;
+                const bool n1 = tile_id(s + 1) >= 0;
                 if (n1) load_rq(rq[2], strip_pixel(tile_id(s + 1), pw));
                 pair_strip(pw, strip_pixel(t, pw), rq[0]);
                 cbar();
@@ -431,9 +453,9 @@ __global__ void __launch_bounds__(512, 1) k_c3pair(C3PairArgs a, int tiles_w, in
                 pair_strip(4 + pw, strip_pixel(t, 4 + pw), rq[1]);
                 cbar();
             }
-            if (s + 1 < nmine) {  // tile s + 1 from buffers 2 / 3, tile s + 2's into 0 / 1
+            if (tile_id(s + 1) >= 0) {  // tile s + 1 from buffers 2 / 3, tile s + 2's into 0 / 1
                 const int t = tile_id(s + 1);
-                const bool n2 = s + 2 < nmine;
+                const bool n2 = tile_id(s + 2) >= 0;
                 if (n2) load_rq(rq[0], strip_pixel(tile_id(s + 2), pw));
                 pair_strip(pw, strip_pixel(t, pw), rq[2]);
                 cbar();
@@ -456,7 +478,7 @@ extern "C" int rr_conv3x3_pair(const void* t1, int n, int h, int w, const void* 
                                const float* shift3, const void* residual, const void* xp, const void* wp,
                                const float* scalep, const float* shiftp, int act3, float slope3, const void* w1,
                                const float* scale1, const float* shift1, int c_out, int act1, float slope1, void* y,
-                               void* z, int dtype, void* stream) {
+                               void* z, int* tile_queue, int dtype, void* stream) {
     if (dtype != RR_BF16 && dtype != RR_F16) return fail(RR_EINVAL, "rr_conv3x3_pair: dtype (bf16 / fp16)");
     if (!t1 || !w33 || !scale2 || !shift2 || !w3 || !scale3 || !shift3 || !w1 || !scale1 || !shift1 || !y || !z)
         return fail(RR_EINVAL, "rr_conv3x3_pair: null pointer");
@@ -469,6 +491,7 @@ extern "C" int rr_conv3x3_pair(const void* t1, int n, int h, int w, const void* 
     if ((long long)n * h * w * 64 * 2 >= (1ll << 31)) return fail(RR_EINVAL, "rr_conv3x3_pair: t1 over 2 GiB (split the batch)");
     for (const void* p : {t1, w33, w3, residual, xp, wp, w1, (const void*)y, (const void*)z})
         if ((uintptr_t)p & 15) return fail(RR_EINVAL, "rr_conv3x3_pair: 16-byte alignment required");
+    if ((uintptr_t)tile_queue & 3) return fail(RR_EINVAL, "rr_conv3x3_pair: tile_queue alignment");
     for (int act : {act2, act3, act1})
         if (act != RR_ACT_IDENTITY && act != RR_ACT_LEAKY) return fail(RR_EINVAL, "rr_conv3x3_pair: activation");
     C3PairArgs a;
@@ -477,7 +500,7 @@ extern "C" int rr_conv3x3_pair(const void* t1, int n, int h, int w, const void* 
     a.xp = (const bf16_t*)xp; a.wp = (const bf16_t*)wp; a.sp = scalep; a.hp = shiftp;
     a.w1 = (const bf16_t*)w1; a.s1 = scale1; a.h1 = shift1; a.y = (bf16_t*)y; a.z = (bf16_t*)z;
     a.n = n; a.h = h; a.w = w; a.act2 = act2; a.act3 = act3; a.act1 = act1;
-    a.slope2 = slope2; a.slope3 = slope3; a.slope1 = slope1;
+    a.slope2 = slope2; a.slope3 = slope3; a.slope1 = slope1; a.queue = tile_queue;
     const int tiles_w = w / 32, tiles_hw = (h / 4) * tiles_w;
     const long long ntl = (long long)n * tiles_hw;
     if (ntl >= (1ll << 31)) return fail(RR_EINVAL, "rr_conv3x3_pair: too many tiles");

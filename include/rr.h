@@ -122,13 +122,16 @@ int rr_conv1x1_pair(const void* x, long long p, int c_in, const void* w3, const 
  * matrix work runs beside the boundary's memory traffic.  shortcut = residual ([p][256]) or,
  * with residual == NULL, the projection proj_bn(proj_conv(xp)) (c_out 64).  t1 [n][h][w][64],
  * h % 4 == 0, w % 32 == 0; y / z bit-identical to the unfused launches (the 3x3 kernel +
- * rr_conv1x1_pair).  RR_EINVAL for other shapes (the caller runs those launches instead). */
+ * rr_conv1x1_pair).  RR_EINVAL for other shapes (the caller runs those launches instead).
+ * tile_queue: 8 ints, zero on entry, used as per-XCD tile counters (blocks that start late
+ * take fewer tiles; the kernel leaves them non-zero, so one zeroed array per launch), or
+ * NULL for the static tile walk; the results do not depend on it. */
 int rr_conv3x3_pair(const void* t1, int n, int h, int w, const void* w33, const float* scale2,
                     const float* shift2, int act2, float slope2, const void* w3, const float* scale3,
                     const float* shift3, const void* residual, const void* xp, const void* wp,
                     const float* scalep, const float* shiftp, int act3, float slope3, const void* w1,
                     const float* scale1, const float* shift1, int c_out, int act1, float slope1, void* y,
-                    void* z, int dtype, void* stream);
+                    void* z, int* tile_queue, int dtype, void* stream);
 
 /* 3x3/s2/p1 style max pooling, NHWC.  Replaces nn.MaxPool2d(3, stride=2,
  * padding=1) of the stem (cirtorch/backbones/resnet.py:65). */

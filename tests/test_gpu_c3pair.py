@@ -1,7 +1,8 @@
 """The fused 256-channel-stage block (rr_conv3x3_pair: conv2 3x3 + conv3 + shortcut of block i and
 conv1 of block i + 1, cirtorch/backbones/misc.py:163-203, in one launch with t2 kept on chip) vs
 the two unfused launches (the 3x3 kernel, then rr_conv1x1_pair): y and z bit-identical — same
-MFMA K-step order and the same 16-bit rounding of t2 — and vs a float64 restatement.  GPU only."""
+MFMA K-step order and the same 16-bit rounding of t2 — for the dynamic (per-XCD tile queue) and
+the static tile walk, and vs a float64 restatement.  GPU only."""
 
 import pytest
 import torch
@@ -37,7 +38,11 @@ def _case(cuda, dt, n, h, w, c_out, proj, seed):
     pj = (xe, wpp, spd, hpd) if proj else None
     r = None if proj else re
     y, z = ops.conv3x3_pair(t1e, w33p, s2d, h2d, True, 0.01, w3p, s3d, h3d, r, True, 0.01,
-                            w1p, s1d, h1d, c_out, True, 0.01, proj=pj)
+                            w1p, s1d, h1d, c_out, True, 0.01, proj=pj, dynamic=True)
+    # the static tile walk: same bits
+    ys, zs = ops.conv3x3_pair(t1e, w33p, s2d, h2d, True, 0.01, w3p, s3d, h3d, r, True, 0.01,
+                              w1p, s1d, h1d, c_out, True, 0.01, proj=pj, dynamic=False)
+    assert torch.equal(y, ys) and torch.equal(z, zs)
     # the unfused launches
     t2 = ops.conv2d_fused(t1e, w33p, 3, 3, 1, 1, 64, s2d, h2d, leaky=True, slope=0.01, perm32=True)
     y2, z2 = ops.conv1x1_pair(t2, w3p, s3d, h3d, r, True, 0.01, w1p, s1d, h1d, c_out, True, 0.01, proj=pj)

@@ -46,9 +46,9 @@ def main():
             return ops.conv1x1_pair(t2, w3, one(256), zero(256), r, True, 0.01, w1, one(c1), zero(c1), c1, True, 0.01,
                                     proj=pj)
 
-        def fused():
+        def fused(dyn=True):
             return ops.conv3x3_pair(t1, w33, one(64), zero(64), True, 0.01, w3, one(256), zero(256), r, True, 0.01,
-                                    w1, one(c1), zero(c1), c1, True, 0.01, proj=pj)
+                                    w1, one(c1), zero(c1), c1, True, 0.01, proj=pj, dynamic=dyn)
 
         t2 = ops.conv2d_fused(t1, w33, 3, 3, 1, 1, 64, one(64), zero(64), leaky=True, perm32=True)
 
@@ -59,9 +59,9 @@ def main():
         ya, za = unfused()
         yb, zb = fused()
         same = torch.equal(ya, yb) and torch.equal(za, zb)
-        tu, tf, tp = timed(unfused), timed(fused), timed(pair_only)
-        print("block %-8s n=%d: unfused %.1f us (pair alone %.1f), fused %.1f us (%.3fx; %.3f of the pair alone), "
-              "bit-identical %s" % (name, n, tu, tp, tf, tu / tf, tf / tp, same), flush=True)
+        tu, tf, tp, ts = timed(unfused), timed(fused), timed(pair_only), timed(lambda: fused(False))
+        print("block %-8s n=%d: unfused %.1f us (pair alone %.1f), fused %.1f us (%.3fx; %.3f of the pair alone; "
+              "static walk %.1f), bit-identical %s" % (name, n, tu, tp, tf, tu / tf, tf / tp, ts, same), flush=True)
 
 
 if __name__ == "__main__":
