@@ -1672,6 +1672,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm8a(ConvArgs a, int tiles_p, int 
 static int g_gemm8 = -1;  // rr_set_tuning(RR_TUNE_GEMM8) / RR_GEMM8: 0 off, 1 auto (default), 2 force where legal
 static bool g_gemm8_tile = false;  // RR_TUNE_GEMM8 value | 4: one block per tile instead of persistent blocks
 static bool g_gemm8_pmajor = true;  // RR_TUNE_GEMM8 value | 64: conv tiles channel-major
+static bool g_gemm8_short_persist = true;  // RR_TUNE_GEMM8 value | 512: short-K 1x1 convs one block per tile
 
 // 16-bit operands, 1x1 or tap-uniform im2col, an even number of 64-deep
 // K-steps, 31-bit operand offsets, and (auto) enough 256 x 256 tiles to fill
@@ -1717,7 +1718,7 @@ static bool try_gemm8(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
         // (128 x R50 layers, same box: K = 512 540 -> 521 / 579 -> 552 us, K = 1024
         // neutral to -8 us; K = 2048 and the 3x3s measured slower, so they stay one block
         // per tile).
-        const bool short_k1 = k1 && a.kp / 64 <= 16 && !(a.flags & RR_CONV_RESIDUAL);
+        const bool short_k1 = g_gemm8_short_persist && k1 && a.kp / 64 <= 16 && !(a.flags & RR_CONV_RESIDUAL);
         const bool persist = !g_gemm8_tile && (g_gemm8 == 2 || !std::is_same<T, TO>::value ||
                                                (std::is_same<T, TO>::value && short_k1));
         // (a grid below 8 blocks would leave some XCD's tile range without a block)
@@ -1898,6 +1899,7 @@ void set_gemm_tuning(int key, int value) {
         g_gemm8s = !(value >= 0 && (value & 32));
         g_gemm8_tile = value >= 0 && (value & 4);
         g_gemm8_pmajor = !(value >= 0 && (value & 64));
+        g_gemm8_short_persist = !(value >= 0 && (value & 512));
         g_gemm8a_tile = value >= 0 && (value & 128);
         value = value < 0 ? 0 : value & 3;
         g_gemm8 = value > 2 ? 2 : value;
