@@ -120,3 +120,35 @@ def test_backbone_block_fusion_bit_identical(cuda, prec, monkeypatch):
         assert len(calls) == 3
     for k in fused:
         assert torch.equal(fused[k], plain[k]), k
+
+
+def test_conv3x3_pair_dynamic_queue_under_contention(cuda):
+    """The per-XCD tile queue hands tiles to whichever blocks run first: with another stream's
+    long kernels holding part of the chip (as the bench step's search does), the blocks take
+    different tile sets, and y / z stay bit-identical to the static walk."""
+    from cirtorch import _ops as ops
+    dt = torch.float16
+    n, h, w = 24, 48, 128
+    g = torch.Generator(device=cuda).manual_seed(11)
+    rn = lambda *s, sc=0.5: (torch.randn(*s, generator=g, device=cuda) * sc).to(dt)  # noqa: E731
+    t1, res = rn(n, h, w, 64), rn(n, h, w, 256)
+    w33 = ops.pack_conv_weights(torch.randn(64, 64, 3, 3, generator=g, device=cuda) * 0.06, 64, dt, perm32=True)
+    w3, w1 = rn(256, 64, sc=0.1), rn(128, 256, sc=0.05)
+    one = lambda c: torch.ones(c, device=cuda)  # noqa: E731
+    zero = lambda c: torch.zeros(c, device=cuda)  # noqa: E731
+
+    def run(dyn):
+        return ops.conv3x3_pair(t1, w33, one(64), zero(64), True, 0.01, w3, one(256), zero(256), res, True, 0.01,
+                                w1, one(128), zero(128), 128, True, 0.01, dynamic=dyn)
+
+    ys, zs = run(False)
+    a = torch.randn(4096, 4096, device=cuda, dtype=dt)
+    side = torch.cuda.Stream(device=cuda)
+    for _ in range(3):
+        side.wait_stream(torch.cuda.current_stream(cuda))
+        with torch.cuda.stream(side):
+            for _ in range(4):
+                a = (a @ a).clamp_(-1, 1)  # long kernels on a second stream
+        y, z = run(True)
+        torch.cuda.synchronize()
+        assert torch.equal(y, ys) and torch.equal(z, zs)
