@@ -152,3 +152,27 @@ def test_conv3x3_pair_dynamic_queue_under_contention(cuda):
         y, z = run(True)
         torch.cuda.synchronize()
         assert torch.equal(y, ys) and torch.equal(z, zs)
+
+
+@pytest.mark.parametrize("c_out,proj", [(64, True), (64, False), (128, False)])
+def test_conv3x3_pair_bench_shape(cuda, c_out, proj):
+    """The bench's mod2 map (192 x 256 pixels, 8 images: 3072 tiles, ~12 per block, both tile
+    walks): y / z bit-identical to the unfused launches at full spatial size."""
+    from cirtorch import _ops as ops
+    dt = torch.float16
+    n, h, w = 8, 192, 256
+    g = torch.Generator(device=cuda).manual_seed(c_out + proj)
+    rn = lambda *s, sc=0.5: (torch.randn(*s, generator=g, device=cuda) * sc).to(dt)  # noqa: E731
+    t1, xin, res = rn(n, h, w, 64), rn(n, h, w, 64), rn(n, h, w, 256)
+    w33 = ops.pack_conv_weights(torch.randn(64, 64, 3, 3, generator=g, device=cuda) * 0.06, 64, dt, perm32=True)
+    w3, wp, w1 = rn(256, 64, sc=0.1), rn(256, 64, sc=0.1), rn(c_out, 256, sc=0.05)
+    aff = lambda c: (torch.rand(c, generator=g, device=cuda) + 0.5, torch.randn(c, generator=g, device=cuda) * 0.1)  # noqa: E731
+    (s2, h2), (s3, h3), (sp, hp), (s1, h1) = aff(64), aff(256), aff(256), aff(c_out)
+    pj = (xin, wp, sp, hp) if proj else None
+    r = None if proj else res
+    t2 = ops.conv2d_fused(t1, w33, 3, 3, 1, 1, 64, s2, h2, leaky=True, slope=0.01, perm32=True)
+    y2, z2 = ops.conv1x1_pair(t2, w3, s3, h3, r, True, 0.01, w1, s1, h1, c_out, True, 0.01, proj=pj)
+    for dyn in (True, False):
+        y, z = ops.conv3x3_pair(t1, w33, s2, h2, True, 0.01, w3, s3, h3, r, True, 0.01, w1, s1, h1, c_out, True, 0.01,
+                                proj=pj, dynamic=dyn)
+        assert torch.equal(y, y2) and torch.equal(z, z2), dyn
