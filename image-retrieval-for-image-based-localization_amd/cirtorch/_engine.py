@@ -43,7 +43,7 @@ _SIGS = {
     "rr_conv2d_fused": ([_vp, _vp, _vp, _vp, _vp, _vp, ctypes.POINTER(ConvDesc), _i, _i, _vp], _i),
     "rr_conv1x1_pair": ([_vp, _ll, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _i, _f, _vp, _vp, _vp, _i, _i, _f,
                          _vp, _vp, _i, _vp], _i),
-    "rr_conv3x3_pair": ([_vp, _i, _i, _i, _vp, _vp, _vp, _i, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _f,
+    "rr_conv3x3_pair": ([_vp, _i, _i, _i, _vp, _vp, _vp, _i, _f, _vp, _vp, _vp, _i, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _f,
                          _vp, _vp, _vp, _i, _i, _f, _vp, _vp, _vp, _i, _vp], _i),
     "rr_pack_conv_weights": ([_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _vp], _i),
     "rr_stem_pack_weights": ([_vp, _i, _i, _i, _i, _vp, _i, _vp], _i),

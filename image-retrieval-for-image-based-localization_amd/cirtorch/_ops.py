@@ -110,7 +110,7 @@ def conv1x1_pair(x, w3, scale3, shift3, residual, leaky3, slope3, w1, scale1, sh
 
 
 def conv3x3_pair(t1, w33, scale2, shift2, leaky2, slope2, w3, scale3, shift3, residual, leaky3, slope3,
-                 w1, scale1, shift1, c_out, leaky1, slope1, proj=None, dynamic=None):
+                 w1, scale1, shift1, c_out, leaky1, slope1, proj=None, dynamic=None, conv1=None):
     """One whole bottleneck block of the 256-channel stage plus the next block's conv1 in one
     launch (cirtorch/backbones/misc.py:163-203): t2 = act2(conv3x3(t1, w33)*scale2 + shift2),
     y = act3(conv1x1(t2, w3)*scale3 + shift3 + shortcut), z = act1(conv1x1(y, w1)*scale1 + shift1);
@@ -118,7 +118,9 @@ def conv3x3_pair(t1, w33, scale2, shift2, leaky2, slope2, w3, scale3, shift3, re
     the block's projection.  t1: [N, H, W, 64] bf16 / fp16 with H % 4 == 0 and W % 32 == 0, PERM32
     weights; returns (y [N, H, W, 256], z [N, H, W, c_out]), bit-identical to the 3x3 launch
     followed by conv1x1_pair.  dynamic (default: RR_C3PAIR_QUEUE != "0"): per-XCD tile counters
-    (a zeroed 8-int array per launch) instead of the static tile walk — same results."""
+    (a zeroed 8-int array per launch) instead of the static tile walk — same results.
+    conv1=(w0, scale0, shift0, leaky0, slope0) (projection form, the stage's first block): t1 is
+    the block input x (pass it as proj's xp too) and the block's conv1 runs in the launch."""
     E.require_gpu(t1, w33, w3, residual, w1)
     n, h, w, c = t1.shape
     assert c == 64 and t1.is_contiguous() and tuple(w33.shape) == (64, 576) and tuple(w3.shape) == (256, 64)
@@ -136,7 +138,12 @@ def conv3x3_pair(t1, w33, scale2, shift2, leaky2, slope2, w3, scale3, shift3, re
     if dynamic is None:
         dynamic = os.environ.get("RR_C3PAIR_QUEUE", "1") != "0"
     queue = torch.zeros(8, dtype=torch.int32, device=t1.device) if dynamic else None
-    E.check(E.lib().rr_conv3x3_pair(E.ptr(t1), n, h, w, E.ptr(w33), E.ptr(scale2), E.ptr(shift2), act(leaky2),
+    w0, s0, h0, leaky0, slope0 = conv1 if conv1 is not None else (None, None, None, False, 0.0)
+    if conv1 is not None:
+        E.require_gpu(w0, s0, h0)
+        assert proj is not None and tuple(w0.shape) == (64, 64)
+    E.check(E.lib().rr_conv3x3_pair(E.ptr(t1), n, h, w, E.ptr(w0), E.ptr(s0), E.ptr(h0), act(leaky0), float(slope0),
+                                    E.ptr(w33), E.ptr(scale2), E.ptr(shift2), act(leaky2),
                                     float(slope2), E.ptr(w3), E.ptr(scale3), E.ptr(shift3), E.ptr(residual),
                                     E.ptr(xp), E.ptr(wp), E.ptr(sp), E.ptr(hp), act(leaky3), float(slope3),
                                     E.ptr(w1), E.ptr(scale1), E.ptr(shift1), c_out, act(leaky1), float(slope1),

@@ -217,16 +217,22 @@ class ResNet(nn.Module):
             res = t if proj is None else (None if fuse_proj else self._conv(t, proj))
             # the whole block (3x3 + boundary pair) in one launch: the 3x3 is not run on its own
             block = pair and self._c3pairable(t, steps, nxt, fuse_proj)
+            # the stage's first block: its conv1 (64 -> 64 on the block input) in the same launch
+            conv1 = block and fuse_proj and pending is None and self._conv1_fusable(t, steps[0])
             y = t
             for j, st in enumerate(steps[:-2] if block else steps[:-1]):
+                if conv1:
+                    break
                 y = pending if (j == 0 and pending is not None) else self._conv(y, st)
             pending = None
             if block:
                 mid, last = steps[-2], steps[-1]
+                c1 = steps[0]
                 t, pending = _ops.conv3x3_pair(y, mid.w, mid.scale, mid.shift, mid.leaky, mid.slope,
                                                last.w, last.scale, last.shift, res, last.leaky, last.slope,
                                                nxt.w, nxt.scale, nxt.shift, nxt.c_out, nxt.leaky, nxt.slope,
-                                               proj=(t, proj.w, proj.scale, proj.shift) if fuse_proj else None)
+                                               proj=(t, proj.w, proj.scale, proj.shift) if fuse_proj else None,
+                                               conv1=(c1.w, c1.scale, c1.shift, c1.leaky, c1.slope) if conv1 else None)
             elif pair:
                 last = steps[-1]
                 t, pending = _ops.conv1x1_pair(y, last.w, last.scale, last.shift, res, last.leaky, last.slope,
@@ -272,6 +278,15 @@ class ResNet(nn.Module):
                 and tuple(mid.w.shape) == (64, 576) and last.c_out == 256 and last.w.shape[1] == 64
                 and nxt.c_out in ((64,) if fuse_proj else (64, 128)) and h % 4 == 0 and w % 32 == 0
                 and n * h * w * 64 * 2 < 2 ** 31)
+
+    @staticmethod
+    def _conv1_fusable(t, st):
+        """the block's conv1 is a 1x1 / stride-1 64 -> 64 PERM32 conv of its 64-channel input.
+        Opt-in (RR_C3PAIR_CONV1=1): measured -2 % for that block isolated but neutral in the
+        bench step (the extra barrier per tile slows the block by about what conv1's own
+        launch cost; profiles/r05_ab/r05cv_*), so conv1 stays its own launch by default."""
+        return (os.environ.get("RR_C3PAIR_CONV1", "0") == "1" and st.kh == 1 and st.kw == 1 and st.stride == 1
+                and st.pad == 0 and st.perm and st.c_out == 64 and tuple(st.w.shape) == (64, 64) and t.shape[-1] == 64)
 
     def _pairable(self, last, nxt):
         """conv3 of a bottleneck followed by a stride-1 1x1 conv1 of the next block: one fused

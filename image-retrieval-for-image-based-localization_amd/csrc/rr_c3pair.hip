@@ -73,7 +73,9 @@ __device__ __forceinline__ void cpin(uint4& v) { asm volatile("" : "+v"(v.x), "+
 }  // namespace
 
 struct C3PairArgs {
-    const bf16_t* t1;          // [n][h][w][64]: conv1 output of block i
+    const bf16_t* t1;          // [n][h][w][64]: conv1 output of block i (CONV1: the block input)
+    const bf16_t* w0;          // CONV1: conv1 of block i, [64][64] PERM32 rows
+    const float *s0, *h0;      // CONV1: folded bn1
     const bf16_t* w33;         // [64][576] PERM32 rows, k = tap * 64 + ci
     const float *s33, *h33;    // folded bn2
     const bf16_t* w3;          // [256][64] PERM32 rows
@@ -88,14 +90,19 @@ struct C3PairArgs {
     bf16_t* z;                 // [P][C1]
     int* queue;                // 8 zeroed per-XCD tile counters (dynamic walk) or NULL (static)
     int n, h, w;
-    int act2, act3, act1;
-    float slope2, slope3, slope1;
+    int act2, act3, act1, act0;
+    float slope2, slope3, slope1, slope0;
 };
 
 namespace {
 
-template <int C1, bool PROJ, typename HT>
+// CONV1 (the stage's first block, PROJ): the patch DMA brings the block input x, and the 3x3
+// role turns it into t1 = act0(W0 x s0 + h0) in place (k_stream1x1's K order and rounding;
+// slots outside the image back to the 3x3's zero padding) before its 3x3 — one more barrier
+// per tile, and conv1's own launch (x read, t1 written and re-read) is gone.
+template <int C1, bool PROJ, typename HT, bool CONV1 = false>
 __global__ void __launch_bounds__(512, 1) k_c3pair(C3PairArgs a, int tiles_w, int tiles_hw, int ntiles) {
+    static_assert(!CONV1 || PROJ, "conv1 in the launch: the stage's first block only");
     constexpr int TH = 4, TW = 32, TP = TH * TW, PITCH = 40;     // 4 x 32 tile; patch rows 40 slots apart
     constexpr int NSLOT = (TH + 2) * PITCH, NP = NSLOT / 8;      // 240 slots, 30 pieces of 8 slots (1 KiB)
     constexpr int PCW = TW + 2;                                  // 34 patch columns used
@@ -109,6 +116,8 @@ __global__ void __launch_bounds__(512, 1) k_c3pair(C3PairArgs a, int tiles_w, in
     __shared__ __attribute__((aligned(16))) char sWp[PROJ ? C3 * K3 * 2 : 16];
     __shared__ __attribute__((aligned(16))) float sS3[C3], sH3[C3], sS1[C1], sH1[C1], sS2[64], sH2[64];
     __shared__ __attribute__((aligned(16))) float sSp[PROJ ? C3 : 4], sHp[PROJ ? C3 : 4];
+    __shared__ __attribute__((aligned(16))) char sW0[CONV1 ? 64 * 64 * 2 : 16];
+    __shared__ __attribute__((aligned(16))) float sS0[CONV1 ? 64 : 4], sH0[CONV1 ? 64 : 4];
     __shared__ int sTile[4];  // tile of step s in slot s & 3 (-1: none), fetched three steps ahead
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -142,7 +151,16 @@ __global__ void __launch_bounds__(512, 1) k_c3pair(C3PairArgs a, int tiles_w, in
     if (tid < 64) {
         sS2[tid] = a.s33[tid];
         sH2[tid] = a.h33[tid];
+        if constexpr (CONV1) {
+            sS0[tid] = a.s0[tid];
+            sH0[tid] = a.h0[tid];
+        }
     }
+    if constexpr (CONV1)
+        for (int i = tid; i < 64 * 64 / 8; i += 512) {
+            const int r = i / 8, c = i - r * 8;
+            *reinterpret_cast<uint4*>(sW0 + cwswz<64>(r, c)) = reinterpret_cast<const uint4*>(a.w0)[i];
+        }
     const int wc = wave & 1, wpx = (wave >> 1) & 1;  // 3x3 role: channel half, pixel half
 
     // ---- this block's tiles.  Static: k_c3w64's XCD-contiguous walk.  Dynamic (a.queue):
@@ -208,8 +226,9 @@ __global__ void __launch_bounds__(512, 1) k_c3pair(C3PairArgs a, int tiles_w, in
         // fragment address bases (pixel fragment j, tap column dx, half-step hs), derived per
         // tile from an opaque copy of the lane's column: live only across this loop (24 VGPRs),
         // not across the whole tile walk beside the 144 weight VGPRs
-        int lc = r16;
-        asm volatile("" : "+v"(lc));
+        int lc;  // the lane's column, recomputed per tile (not a register live across the walk)
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lc));
+        lc &= 15;
         const char* base[FN][3][2];
 #pragma unroll
         for (int j = 0; j < FN; ++j)
@@ -234,6 +253,61 @@ __global__ void __launch_bounds__(512, 1) k_c3pair(C3PairArgs a, int tiles_w, in
             for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
                 for (int j = 0; j < FN; ++j) acc[ii][j] = H16<HT>::mfma(areg[ii][s], fb[j], acc[ii][j]);
+        }
+    };
+    // CONV1: the patch (block input x) -> t1 in place, one 16-slot fragment per step, fragments
+    // wave, wave + 4, ... (15 per patch): t1 = act0(W0 x s0 + h0) with k_stream1x1's MFMA order
+    // (K-steps 0, 1; channel pairs 32 i2 + 8 kq) and rounding; slots outside the image (and
+    // the unused pitch columns) get 0, the 3x3's zero padding
+    auto convert_patch = [&](int t) __attribute__((always_inline)) {
+        if constexpr (CONV1) {
+            int img, oh0, ow0;
+            tile_org(t, img, oh0, ow0);
+            const bool leaky0 = a.act0 == RR_ACT_LEAKY;
+            for (int f = wave; f < NP * 8 / 16; f += 4) {
+                int q = f * 16 + r16;
+                asm volatile("" : "+v"(q));
+                const int pr = q / PITCH, pc = q - pr * PITCH;
+                const int hh = oh0 - 1 + pr, ww = ow0 - 1 + pc;
+                const bool valid = pc < PCW && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W;
+                char* slot = sPatch + q * 128;
+                uint4 bx[2];
+#pragma unroll
+                for (int kk = 0; kk < 2; ++kk)
+                    bx[kk] = *reinterpret_cast<const uint4*>(slot + (((4 * kk + kq) ^ (q & 7)) << 4));
+                h16_f32x4_t c0[4];
+#pragma unroll
+                for (int ii = 0; ii < 4; ++ii) c0[ii] = (h16_f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+                    for (int ii = 0; ii < 4; ++ii) {
+                        const uint4 av = *reinterpret_cast<const uint4*>(sW0 + cwswz<64>(ii * 16 + r16, kk * 4 + kq));
+                        c0[ii] = H16<HT>::mfma(av, bx[kk], c0[ii]);
+                    }
+#pragma unroll
+                for (int i2 = 0; i2 < 2; ++i2) {
+                    const int c = 32 * i2 + 8 * kq;
+                    float v[8];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        v[r] = c0[2 * i2][r] * sS0[c + r] + sH0[c + r];
+                        v[4 + r] = c0[2 * i2 + 1][r] * sS0[c + 4 + r] + sH0[c + 4 + r];
+                    }
+                    if (leaky0) {
+#pragma unroll
+                        for (int r = 0; r < 8; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * a.slope0;
+                    }
+                    uint4 o = make_uint4(0u, 0u, 0u, 0u);
+                    if (valid) {
+                        o.x = H16<HT>::pack2(v[0], v[1]);
+                        o.y = H16<HT>::pack2(v[2], v[3]);
+                        o.z = H16<HT>::pack2(v[4], v[5]);
+                        o.w = H16<HT>::pack2(v[6], v[7]);
+                    }
+                    *reinterpret_cast<uint4*>(slot + (((4 * i2 + kq) ^ (q & 7)) << 4)) = o;
+                }
+            }
         }
     };
     // bn2 + act, 8 consecutive channels per lane -> the t2 tile (16-B chunk ^ (pixel & 7))
@@ -407,6 +481,10 @@ __global__ void __launch_bounds__(512, 1) k_c3pair(C3PairArgs a, int tiles_w, in
         patch_dma(tile_id(0), true);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         cbar();
+        if constexpr (CONV1) {
+            convert_patch(tile_id(0));
+            cbar();
+        }
         conv();
         if (wpx == 0) store_t2();
         cbar();  // every 3x3 wave is done with patch 0
@@ -417,6 +495,10 @@ __global__ void __launch_bounds__(512, 1) k_c3pair(C3PairArgs a, int tiles_w, in
             const bool more = tile_id(s + 1) >= 0;
             // phase A: tile s's strips 4-7 (lower pixel half), then tile s + 1's 3x3
             if (wpx == 1) store_t2();
+            if constexpr (CONV1) {
+                if (more) convert_patch(tile_id(s + 1));
+                cbar();
+            }
             if (more) conv();
             cbar();
             // phase B: tile s + 1's strips 0-3 (upper pixel half), tile s + 2's patch
@@ -440,6 +522,7 @@ __global__ void __launch_bounds__(512, 1) k_c3pair(C3PairArgs a, int tiles_w, in
         load_rq(rq[0], strip_pixel(tile_id(0), pw));
         load_rq(rq[1], strip_pixel(tile_id(0), 4 + pw));
         cbar();
+        if constexpr (CONV1) cbar();  // the 3x3 role's conv1 of patch 0
         cbar();
         cbar();
         for (int s = 0; tile_id(s) >= 0; s += 2) {
@@ -447,6 +530,7 @@ __global__ void __launch_bounds__(512, 1) k_c3pair(C3PairArgs a, int tiles_w, in
                 const int t = tile_id(s);
                 const bool n1 = tile_id(s + 1) >= 0;
                 if (n1) load_rq(rq[2], strip_pixel(tile_id(s + 1), pw));
+                if constexpr (CONV1) cbar();  // the 3x3 role's conv1 of the next patch
                 pair_strip(pw, strip_pixel(t, pw), rq[0]);
                 cbar();
                 if (n1) load_rq(rq[3], strip_pixel(tile_id(s + 1), 4 + pw));
@@ -457,6 +541,7 @@ __global__ void __launch_bounds__(512, 1) k_c3pair(C3PairArgs a, int tiles_w, in
                 const int t = tile_id(s + 1);
                 const bool n2 = tile_id(s + 2) >= 0;
                 if (n2) load_rq(rq[0], strip_pixel(tile_id(s + 2), pw));
+                if constexpr (CONV1) cbar();
                 pair_strip(pw, strip_pixel(t, pw), rq[2]);
                 cbar();
                 if (n2) load_rq(rq[1], strip_pixel(tile_id(s + 2), 4 + pw));
@@ -473,7 +558,8 @@ __global__ void __launch_bounds__(512, 1) k_c3pair(C3PairArgs a, int tiles_w, in
 
 using namespace rr;
 
-extern "C" int rr_conv3x3_pair(const void* t1, int n, int h, int w, const void* w33, const float* scale2,
+extern "C" int rr_conv3x3_pair(const void* t1, int n, int h, int w, const void* w0, const float* scale0,
+                               const float* shift0, int act0, float slope0, const void* w33, const float* scale2,
                                const float* shift2, int act2, float slope2, const void* w3, const float* scale3,
                                const float* shift3, const void* residual, const void* xp, const void* wp,
                                const float* scalep, const float* shiftp, int act3, float slope3, const void* w1,
@@ -487,6 +573,10 @@ extern "C" int rr_conv3x3_pair(const void* t1, int n, int h, int w, const void* 
         return fail(RR_EINVAL, "rr_conv3x3_pair: either residual or the projection (xp, wp, scalep, shiftp)");
     if (c_out != 64 && c_out != 128) return fail(RR_EINVAL, "rr_conv3x3_pair: c_out 64 or 128");
     if (proj && c_out != 64) return fail(RR_EINVAL, "rr_conv3x3_pair: the projection form takes c_out = 64");
+    const bool conv1 = w0 != nullptr;
+    if (conv1 && (!proj || !scale0 || !shift0 || ((uintptr_t)w0 & 15)))
+        return fail(RR_EINVAL, "rr_conv3x3_pair: conv1 in the launch (w0) needs the projection form, scale0, shift0");
+    if (conv1 && act0 != RR_ACT_IDENTITY && act0 != RR_ACT_LEAKY) return fail(RR_EINVAL, "rr_conv3x3_pair: act0");
     if (n <= 0 || h <= 0 || w <= 0 || h % 4 || w % 32) return fail(RR_EINVAL, "rr_conv3x3_pair: h % 4, w % 32");
     if ((long long)n * h * w * 64 * 2 >= (1ll << 31)) return fail(RR_EINVAL, "rr_conv3x3_pair: t1 over 2 GiB (split the batch)");
     for (const void* p : {t1, w33, w3, residual, xp, wp, w1, (const void*)y, (const void*)z})
@@ -501,6 +591,7 @@ extern "C" int rr_conv3x3_pair(const void* t1, int n, int h, int w, const void* 
     a.w1 = (const bf16_t*)w1; a.s1 = scale1; a.h1 = shift1; a.y = (bf16_t*)y; a.z = (bf16_t*)z;
     a.n = n; a.h = h; a.w = w; a.act2 = act2; a.act3 = act3; a.act1 = act1;
     a.slope2 = slope2; a.slope3 = slope3; a.slope1 = slope1; a.queue = tile_queue;
+    a.w0 = (const bf16_t*)w0; a.s0 = scale0; a.h0 = shift0; a.act0 = act0; a.slope0 = slope0;
     const int tiles_w = w / 32, tiles_hw = (h / 4) * tiles_w;
     const long long ntl = (long long)n * tiles_hw;
     if (ntl >= (1ll << 31)) return fail(RR_EINVAL, "rr_conv3x3_pair: too many tiles");
@@ -511,7 +602,8 @@ extern "C" int rr_conv3x3_pair(const void* t1, int n, int h, int w, const void* 
     hipStream_t s = as_stream(stream);
     auto go = [&](auto hv) {
         using H = decltype(hv);
-        if (proj) hipLaunchKernelGGL((k_c3pair<64, true, H>), g, b, 0, s, a, tiles_w, tiles_hw, (int)ntl);
+        if (conv1) hipLaunchKernelGGL((k_c3pair<64, true, H, true>), g, b, 0, s, a, tiles_w, tiles_hw, (int)ntl);
+        else if (proj) hipLaunchKernelGGL((k_c3pair<64, true, H>), g, b, 0, s, a, tiles_w, tiles_hw, (int)ntl);
         else if (c_out == 64) hipLaunchKernelGGL((k_c3pair<64, false, H>), g, b, 0, s, a, tiles_w, tiles_hw, (int)ntl);
         else hipLaunchKernelGGL((k_c3pair<128, false, H>), g, b, 0, s, a, tiles_w, tiles_hw, (int)ntl);
     };

@@ -123,10 +123,14 @@ int rr_conv1x1_pair(const void* x, long long p, int c_in, const void* w3, const 
  * with residual == NULL, the projection proj_bn(proj_conv(xp)) (c_out 64).  t1 [n][h][w][64],
  * h % 4 == 0, w % 32 == 0; y / z bit-identical to the unfused launches (the 3x3 kernel +
  * rr_conv1x1_pair).  RR_EINVAL for other shapes (the caller runs those launches instead).
+ * w0 (PERM32 [64][64]) or NULL: with w0 (projection form only) t1 is the block's input x and
+ * conv1 + bn1 + act0 of the block (t1 = act0(conv1x1(x, w0) * scale0 + shift0)) runs in the
+ * same launch; pass x as xp too.  Bit-identical to rr_conv2d_fused of conv1 first.
  * tile_queue: 8 ints, zero on entry, used as per-XCD tile counters (blocks that start late
  * take fewer tiles; the kernel leaves them non-zero, so one zeroed array per launch), or
  * NULL for the static tile walk; the results do not depend on it. */
-int rr_conv3x3_pair(const void* t1, int n, int h, int w, const void* w33, const float* scale2,
+int rr_conv3x3_pair(const void* t1, int n, int h, int w, const void* w0, const float* scale0,
+                    const float* shift0, int act0, float slope0, const void* w33, const float* scale2,
                     const float* shift2, int act2, float slope2, const void* w3, const float* scale3,
                     const float* shift3, const void* residual, const void* xp, const void* wp,
                     const float* scalep, const float* shiftp, int act3, float slope3, const void* w1,

@@ -88,13 +88,13 @@ int main() {
                            nullptr, 1, 0.01f, fake(), nullptr, nullptr, 64, 1, 0.01f, fake(), fake(), RR_BF16,
                            nullptr) == RR_EINVAL);                                // c_in 32: no fused form
     const float* ff = (const float*)fake();
-    EXPECT(rr_conv3x3_pair(fake(), 2, 18, 64, fake(), ff, ff, 1, 0.01f, fake(), ff, ff, fake(), nullptr, nullptr,
+    EXPECT(rr_conv3x3_pair(fake(), 2, 18, 64, nullptr, nullptr, nullptr, 0, 0.f, fake(), ff, ff, 1, 0.01f, fake(), ff, ff, fake(), nullptr, nullptr,
                            nullptr, nullptr, 1, 0.01f, fake(), ff, ff, 64, 1, 0.01f, fake(), fake(), nullptr, RR_BF16,
                            nullptr) == RR_EINVAL);                                // h % 4
-    EXPECT(rr_conv3x3_pair(fake(), 2, 16, 64, fake(), ff, ff, 1, 0.01f, fake(), ff, ff, nullptr, fake(), fake(),
+    EXPECT(rr_conv3x3_pair(fake(), 2, 16, 64, nullptr, nullptr, nullptr, 0, 0.f, fake(), ff, ff, 1, 0.01f, fake(), ff, ff, nullptr, fake(), fake(),
                            ff, ff, 1, 0.01f, fake(), ff, ff, 128, 1, 0.01f, fake(), fake(), nullptr, RR_F16,
                            nullptr) == RR_EINVAL);                                // projection form with c_out 128
-    EXPECT(rr_conv3x3_pair(fake(), 2, 16, 64, fake(), ff, ff, 1, 0.01f, fake(), ff, ff, fake(), nullptr, nullptr,
+    EXPECT(rr_conv3x3_pair(fake(), 2, 16, 64, nullptr, nullptr, nullptr, 0, 0.f, fake(), ff, ff, 1, 0.01f, fake(), ff, ff, fake(), nullptr, nullptr,
                            nullptr, nullptr, 1, 0.01f, fake(), ff, ff, 64, 1, 0.01f, fake(), fake(), nullptr, RR_F32,
                            nullptr) == RR_EINVAL);                                // 16-bit only
 

@@ -113,13 +113,17 @@ def test_backbone_block_fusion_bit_identical(cuda, prec, monkeypatch):
     orig = _ops.conv3x3_pair
     monkeypatch.setattr(_ops, "conv3x3_pair", lambda *a, **k: calls.append(1) or orig(*a, **k))
     with torch.no_grad():
+        monkeypatch.setenv("RR_C3PAIR_CONV1", "1")  # block 1's conv1 in the launch too (opt-in)
         fused = body(x)
         assert len(calls) == 3  # every block of the stage
+        monkeypatch.setenv("RR_C3PAIR_CONV1", "0")  # block 1's conv1 as its own launch (default)
+        part = body(x)
         monkeypatch.setenv("RR_C3PAIR", "0")
         plain = body(x)
-        assert len(calls) == 3
+        assert len(calls) == 6
     for k in fused:
         assert torch.equal(fused[k], plain[k]), k
+        assert torch.equal(part[k], plain[k]), k
 
 
 def test_conv3x3_pair_dynamic_queue_under_contention(cuda):
@@ -176,3 +180,30 @@ def test_conv3x3_pair_bench_shape(cuda, c_out, proj):
         y, z = ops.conv3x3_pair(t1, w33, s2, h2, True, 0.01, w3, s3, h3, r, True, 0.01, w1, s1, h1, c_out, True, 0.01,
                                 proj=pj, dynamic=dyn)
         assert torch.equal(y, y2) and torch.equal(z, z2), dyn
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("shape", [(2, 12, 32), (9, 28, 64), (4, 192, 256)])
+def test_conv3x3_pair_with_conv1(cuda, dt, shape):
+    """The stage's first block with its conv1 (1x1 64 -> 64 + bn1 + act on the block input) in
+    the same launch: y / z bit-identical to conv1 as its own launch followed by the fused block
+    (t1's zero padding restored outside the image), both tile walks."""
+    from cirtorch import _ops as ops
+    n, h, w = shape
+    g = torch.Generator(device=cuda).manual_seed(h + w)
+    rn = lambda *s, sc=0.5: (torch.randn(*s, generator=g, device=cuda) * sc).to(dt)  # noqa: E731
+    x = rn(n, h, w, 64)
+    w0 = ops.pack_conv_weights(torch.randn(64, 64, 1, 1, generator=g, device=cuda) * 0.15, 64, dt, perm32=True)
+    w33 = ops.pack_conv_weights(torch.randn(64, 64, 3, 3, generator=g, device=cuda) * 0.06, 64, dt, perm32=True)
+    w3, wp, w1 = rn(256, 64, sc=0.1), rn(256, 64, sc=0.1), rn(64, 256, sc=0.05)
+    aff = lambda c: (torch.rand(c, generator=g, device=cuda) + 0.5, torch.randn(c, generator=g, device=cuda) * 0.1)  # noqa: E731
+    (s0, h0), (s2, h2), (s3, h3), (sp, hp), (s1, h1) = aff(64), aff(64), aff(256), aff(256), aff(64)
+    pj = (x, wp, sp, hp)
+    t1 = ops.conv2d_fused(x, w0, 1, 1, 1, 0, 64, s0, h0, leaky=True, slope=0.01, perm32=True)
+    y2, z2 = ops.conv3x3_pair(t1, w33, s2, h2, True, 0.01, w3, s3, h3, None, True, 0.01, w1, s1, h1, 64, True, 0.01,
+                              proj=pj)
+    for dyn in (True, False):
+        y, z = ops.conv3x3_pair(x, w33, s2, h2, True, 0.01, w3, s3, h3, None, True, 0.01, w1, s1, h1, 64, True, 0.01,
+                                proj=pj, dynamic=dyn, conv1=(w0, s0, h0, True, 0.01))
+        assert torch.equal(y, y2), (dyn, (y.float() - y2.float()).abs().max().item())
+        assert torch.equal(z, z2), (dyn, (z.float() - z2.float()).abs().max().item())
