@@ -14,14 +14,17 @@
 //     and the (tap, half-step) MFMA order is k_c3w64's: t2 is bit-identical to it;
 //   * waves 4-7 ("pair role") are k_stream_pair's waves: W3 / W1 (/ Wp) in LDS, one 16-pixel
 //     strip per phase, the strip's t2 read from an LDS tile instead of HBM, the residual (or
-//     the projection's input) prefetched one phase ahead into registers; same MFMA order, so
-//     y and z are bit-identical to the unfused launches;
+//     the projection's input) prefetched two phases ahead into registers, issue priority 1;
+//     same MFMA order, so y and z are bit-identical to the unfused launches;
 //   * two phases per tile, both roles meet at 2 barriers per tile: in phase A the pair role
 //     runs strips 0-3 of tile s while the 3x3 role computes tile s + 1 (its lower pixel half
 //     having first stored tile s's strips 4-7); in phase B the pair role runs strips 4-7 and
 //     the 3x3 role stores tile s + 1's strips 0-3 and loads the patch of tile s + 2 — one
 //     patch buffer and one t2 tile suffice (LDS <= 150 KB with the projection or C1 = 128).
-// Persistent, one 512-thread block per CU over an XCD-contiguous tile range.
+// Persistent, one 512-thread block per CU; XCD x's blocks take tiles of the XCD's contiguous
+// range from a per-XCD atomic counter (or, with no counter array, a static walk).  Optional
+// (CONV1, the stage's first block): the block's own conv1 (1x1 64 -> 64) applied to the patch
+// in LDS, so the launch reads the block input instead of t1.
 #include "rr_internal.h"
 
 namespace rr {
