@@ -27,6 +27,10 @@
 // in LDS, so the launch reads the block input instead of t1.
 #include "rr_internal.h"
 
+#ifndef C3P_IG2
+#define C3P_IG2 1
+#endif
+
 namespace rr {
 
 namespace {
@@ -376,57 +380,73 @@ __global__ void __launch_bounds__(512, 1) k_c3pair(C3PairArgs a, int tiles_w, in
                 bq[kk] = *reinterpret_cast<const uint4*>(sT2 + q * 128 + (((4 * kk + kq) ^ (q & 7)) << 4));
         }
         uint4 yq[NR3];
+        // IG 32-channel groups per step: the projection form has the registers for two, i.e.
+        // four independent W3 and four Wp accumulator chains in flight instead of two
+        constexpr int IG = (PROJ && C3P_IG2) ? 2 : 1;
 #pragma unroll
-        for (int i2 = 0; i2 < NR3; ++i2) {
+        for (int i0 = 0; i0 < NR3; i0 += IG) {
             int abase = 0;
             asm volatile("" : "+v"(abase));  // keep the weight fragments in LDS (no hoisting into VGPRs)
-            h16_f32x4_t acc3[2] = {(h16_f32x4_t){0.f, 0.f, 0.f, 0.f}, (h16_f32x4_t){0.f, 0.f, 0.f, 0.f}};
+            h16_f32x4_t acc3[IG][2], pacc[IG][2];
+#pragma unroll
+            for (int g = 0; g < IG; ++g)
+#pragma unroll
+                for (int hh = 0; hh < 2; ++hh) acc3[g][hh] = pacc[g][hh] = (h16_f32x4_t){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int kk = 0; kk < NK3; ++kk)
 #pragma unroll
-                for (int hh = 0; hh < 2; ++hh) {
-                    const uint4 av = *reinterpret_cast<const uint4*>(sW3 + abase + cwswz<K3>((2 * i2 + hh) * 16 + r16, kk * 4 + kq));
-                    acc3[hh] = H16<HT>::mfma(av, bq[kk], acc3[hh]);
-                }
-            const int c = 32 * i2 + 8 * kq;
-            float v[8];
+                for (int g = 0; g < IG; ++g)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                v[r] = acc3[0][r] * sS3[c + r] + sH3[c + r];
-                v[4 + r] = acc3[1][r] * sS3[c + 4 + r] + sH3[c + 4 + r];
-            }
+                    for (int hh = 0; hh < 2; ++hh) {
+                        const uint4 av = *reinterpret_cast<const uint4*>(sW3 + abase + cwswz<K3>((2 * (i0 + g) + hh) * 16 + r16, kk * 4 + kq));
+                        acc3[g][hh] = H16<HT>::mfma(av, bq[kk], acc3[g][hh]);
+                    }
             if constexpr (PROJ) {  // shortcut = proj_bn(proj_conv(x_in)), kept in f32
-                h16_f32x4_t pacc[2] = {(h16_f32x4_t){0.f, 0.f, 0.f, 0.f}, (h16_f32x4_t){0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
                 for (int kk = 0; kk < NK3; ++kk)
 #pragma unroll
-                    for (int hh = 0; hh < 2; ++hh) {
-                        const uint4 av = *reinterpret_cast<const uint4*>(sWp + abase + cwswz<K3>((2 * i2 + hh) * 16 + r16, kk * 4 + kq));
-                        pacc[hh] = H16<HT>::mfma(av, rv[kk], pacc[hh]);
+                    for (int g = 0; g < IG; ++g)
+#pragma unroll
+                        for (int hh = 0; hh < 2; ++hh) {
+                            const uint4 av = *reinterpret_cast<const uint4*>(sWp + abase + cwswz<K3>((2 * (i0 + g) + hh) * 16 + r16, kk * 4 + kq));
+                            pacc[g][hh] = H16<HT>::mfma(av, rv[kk], pacc[g][hh]);
+                        }
+            }
+#pragma unroll
+            for (int g = 0; g < IG; ++g) {
+                const int i2 = i0 + g;
+                const int c = 32 * i2 + 8 * kq;
+                float v[8];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    v[r] = acc3[g][0][r] * sS3[c + r] + sH3[c + r];
+                    v[4 + r] = acc3[g][1][r] * sS3[c + 4 + r] + sH3[c + 4 + r];
+                }
+                if constexpr (PROJ) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        v[r] += pacc[g][0][r] * sSp[c + r] + sHp[c + r];
+                        v[4 + r] += pacc[g][1][r] * sSp[c + 4 + r] + sHp[c + 4 + r];
                     }
+                } else {
+                    const uint4 qv = rv[i2];
+                    const unsigned w4[4] = {qv.x, qv.y, qv.z, qv.w};
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    v[r] += pacc[0][r] * sSp[c + r] + sHp[c + r];
-                    v[4 + r] += pacc[1][r] * sSp[c + 4 + r] + sHp[c + 4 + r];
+                    for (int r = 0; r < 4; ++r) {
+                        v[2 * r] += H16<HT>::lo(w4[r]);
+                        v[2 * r + 1] += H16<HT>::hi(w4[r]);
+                    }
                 }
-            } else {
-                const uint4 qv = rv[i2];
-                const unsigned w4[4] = {qv.x, qv.y, qv.z, qv.w};
+                if (leaky3) {
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    v[2 * r] += H16<HT>::lo(w4[r]);
-                    v[2 * r + 1] += H16<HT>::hi(w4[r]);
+                    for (int r = 0; r < 8; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * a.slope3;
                 }
+                yq[i2].x = H16<HT>::pack2(v[0], v[1]);
+                yq[i2].y = H16<HT>::pack2(v[2], v[3]);
+                yq[i2].z = H16<HT>::pack2(v[4], v[5]);
+                yq[i2].w = H16<HT>::pack2(v[6], v[7]);
+                st16_once(a.y + p * C3 + c, yq[i2]);
             }
-            if (leaky3) {
-#pragma unroll
-                for (int r = 0; r < 8; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * a.slope3;
-            }
-            yq[i2].x = H16<HT>::pack2(v[0], v[1]);
-            yq[i2].y = H16<HT>::pack2(v[2], v[3]);
-            yq[i2].z = H16<HT>::pack2(v[4], v[5]);
-            yq[i2].w = H16<HT>::pack2(v[6], v[7]);
-            st16_once(a.y + p * C3 + c, yq[i2]);
         }
         h16_f32x4_t zacc[NF1];
 #pragma unroll
