@@ -380,9 +380,9 @@ __global__ void __launch_bounds__(512, 1) k_c3pair(C3PairArgs a, int tiles_w, in
                 bq[kk] = *reinterpret_cast<const uint4*>(sT2 + q * 128 + (((4 * kk + kq) ^ (q & 7)) << 4));
         }
         uint4 yq[NR3];
-        // IG 32-channel groups per step: the projection form has the registers for two, i.e.
-        // four independent W3 and four Wp accumulator chains in flight instead of two
-        constexpr int IG = (PROJ && C3P_IG2) ? 2 : 1;
+        // IG 32-channel groups per step: four independent W3 (and Wp) accumulator chains in
+        // flight instead of two (measured -2 % projection form, -1 % residual forms)
+        constexpr int IG = C3P_IG2 ? 2 : 1;
 #pragma unroll
         for (int i0 = 0; i0 < NR3; i0 += IG) {
             int abase = 0;
