@@ -442,6 +442,9 @@ def knn_topk(db, db_f32, q, q_f32, k, cand=0, idx_offset=0, workspace=None, db_n
     assert db.dtype == q.dtype and db_f32.dtype == torch.float32 and q_f32.dtype == torch.float32
     for t in (db, db_f32, q, q_f32):
         assert t.is_contiguous()
+    if i8_scales is not None and (db_norm_max is None or db.dtype != torch.int8):
+        raise ValueError("knn_topk: i8_scales apply to the certified int8 search only "
+                         "(int8 rows with db_norm_max); they would be ignored here")
     n_db, d = db.shape
     nq = q.shape[0]
     need = knn_workspace_bytes(n_db, nq, d, k, cand, db.dtype)
@@ -455,7 +458,7 @@ def knn_topk(db, db_f32, q, q_f32, k, cand=0, idx_offset=0, workspace=None, db_n
                                     workspace.numel(), E.dtype_code(db.dtype), _st()), "rr_knn_topk")
         return out_s, out_i
     unc = torch.empty(nq, dtype=torch.int32, device=db.device)
-    if i8_scales is not None and db.dtype == torch.int8:
+    if i8_scales is not None:
         qa, da = i8_scales
         assert qa.dtype == torch.float32 and da.dtype == torch.float32 and qa.numel() in (1, nq)
         E.check(E.lib().rr_knn_topk_checked_i8(E.ptr(db), E.ptr(db_f32), n_db, E.ptr(q), E.ptr(q_f32), nq, d, k,

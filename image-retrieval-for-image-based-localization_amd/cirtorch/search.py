@@ -73,6 +73,9 @@ class KnnIndex:
         self.cand = cand
         self.idx_offset = idx_offset
         self._ws = {}   # scratch per stream: searches on different streams never share a slab
+        # the certificate's max row norm, read once here so that no search (and no
+        # profile of one) pays for the norm pass over the database
+        self._norm_max = float(self.db32.norm(dim=1).max().item()) if self.ntotal else 0.0
 
     @property
     def ntotal(self):
@@ -90,9 +93,7 @@ class KnnIndex:
         return ws
 
     def norm_max(self):
-        """largest database row norm (computed once; one device->host read)"""
-        if getattr(self, "_norm_max", None) is None:
-            self._norm_max = float(self.db32.norm(dim=1).max().item()) if self.ntotal else 0.0
+        """largest database row norm (computed when the index is built)"""
         return self._norm_max
 
     def _screen_queries(self, q32):
@@ -101,17 +102,21 @@ class KnnIndex:
             return _ops.quantize_i8(q32, per_row=True, with_scale=True)
         return _ops.cast_screen(q32, self.dtype), None
 
-    def search(self, q_rows, k, verify=False):
+    def search(self, q_rows, k, verify=True):
         """q_rows [Q, D] -> (scores float64 [Q, k], idx int64 [Q, k]) on the current stream.
         An empty shard (ntotal == 0) returns k (-inf, -1) entries per query, which
         the sharded merge drops.
 
-        verify=True certifies the screening margin of every query (the rows left
-        out are provably below the returned k-th score given the screening
-        dtype's error bound) and re-searches uncertain queries — clusters of
-        near-duplicates tighter than the screening error — with float32
-        screening and more candidates; this costs one device->host read per
-        search (no graph capture).
+        verify=True (the default: the reference ranks exactly, scripts/test.py:247-248)
+        certifies the screening margin of every query (the rows left out are provably
+        below the returned k-th score given the screening dtype's error bound) and
+        re-searches uncertain queries — clusters of near-duplicates tighter than the
+        screening error — with float32 screening and more candidates; this costs one
+        device->host read per search, so it cannot be captured in a graph.
+
+        verify=False is the explicit opt-out: the screened candidate pool re-ranked in
+        float64, no certificate (exact unless near-ties straddle the screening cut);
+        graph-capturable.
 
         verify="deferred" returns (scores, idx, pending): the same certificate,
         copied to pinned host memory without a synchronisation; pending.resolve()
@@ -120,6 +125,9 @@ class KnnIndex:
         if q_rows.shape[1] != self.dim:
             raise RuntimeError("KnnIndex.search: queries have D=%d, the database D=%d" % (q_rows.shape[1], self.dim))
         q32 = _pad_cols(q_rows.float().contiguous(), self.d_pad)
+        if verify is True and q32.is_cuda and torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("KnnIndex.search: verify=True reads the certificate back and cannot run "
+                               "inside a graph capture; capture with verify=False (or 'deferred' outside)")
         if self.ntotal == 0 or q32.shape[0] == 0:
             s = torch.full((q32.shape[0], k), float("-inf"), dtype=torch.float64, device=q32.device)
             i = torch.full((q32.shape[0], k), -1, dtype=torch.int64, device=q32.device)
@@ -184,7 +192,7 @@ class KnnIndex:
         for r in range(q32.shape[0]):
             rows = torch.sort(top[r]).values
             sub = KnnIndex(self.db32[rows], "fp32", cand=max(kk, 32))
-            sr, ir = sub.search(q32[r:r + 1], kk)
+            sr, ir = sub.search(q32[r:r + 1], kk, verify=False)   # every row is a candidate
             s[r, :kk], i[r, :kk] = sr[0], rows[ir[0]] + self.idx_offset
         return s, i
 
@@ -228,11 +236,12 @@ class Pending:
         return self.count
 
 
-def knn(vecs, qvecs, k, precision="fp32", cand=0):
-    """vecs D x N, qvecs D x Q (reference layout) -> (ranks k x Q int64, scores k x Q float64)."""
+def knn(vecs, qvecs, k, precision="fp32", cand=0, verify=True):
+    """vecs D x N, qvecs D x Q (reference layout) -> (ranks k x Q int64, scores k x Q float64),
+    certified exact by default (verify=False: the uncertified screen, see KnnIndex.search)."""
     db = _rows(vecs)
     q = _rows(qvecs)
-    s, i = KnnIndex(db, precision, cand).search(q, k)
+    s, i = KnnIndex(db, precision, cand).search(q, k, verify=verify)
     return i.t(), s.t()
 
 
@@ -247,7 +256,8 @@ def rank(vecs, qvecs, precision="fp32", method="auto"):
     rr_rank_full (float64 scores + a stable radix sort), identical order."""
     n = vecs.shape[1]
     if method == "knn" or (method == "auto" and n <= RANK_KNN_MAX):
-        ranks, _ = knn(vecs, qvecs, n, precision=precision, cand=n)
+        # cand = n: every row is re-scored in float64, nothing is screened out to certify
+        ranks, _ = knn(vecs, qvecs, n, precision=precision, cand=n, verify=False)
         return ranks
     db, q = _rows(vecs), _rows(qvecs)
     d_pad = (db.shape[1] + 255) // 256 * 256
@@ -301,18 +311,24 @@ class ShardedIndex:
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.merge = merge or _ops.topk_merge
 
-    def search(self, q_rows, k, verify=False):
-        """merged top-k of the queries (the same on every rank).  verify=True /
+    def search(self, q_rows, k, verify=True):
+        """merged top-k of the queries (the same on every rank).  verify=True (default) /
         "deferred": every shard certifies its own top-k; the flags travel in the
         same all-gather as the lists, so every rank sees the same uncertain set
-        and re-searches it (each shard in float32, then one more exchange) together."""
+        and re-searches it (each shard in float32, then one more exchange) together.
+        verify=False: the uncertified screen."""
         if not verify:
-            s, i = self.local.search(q_rows, k)
+            s, i = self.local.search(q_rows, k, verify=False)
             return (s, i) if self.world == 1 else self.exchange(s, i, k)
         if self.world == 1:
             return self.local.search(q_rows, k, verify=verify)
-        s, i, pl = self.local.search(q_rows, k, verify="deferred")
-        unc = pl.unc if pl.count is None else torch.zeros(q_rows.shape[0], dtype=torch.int32, device=s.device)
+        if self.local.ntotal == 0 or q_rows.shape[0] == 0:
+            # an empty shard certifies trivially: (-inf, -1) lists, no flags
+            s, i = self.local.search(q_rows, k, verify=False)
+            unc = torch.zeros(q_rows.shape[0], dtype=torch.int32, device=s.device)
+        else:
+            # the flags travel in the all-gather: no per-shard Pending (pinned copy + event)
+            s, i, unc = self.local.search_checked(q_rows, k)
         s, i, flags = self.exchange(s, i, k, flags=unc)
 
         def research(bad):
@@ -354,6 +370,6 @@ def mutual_nn(desc1, desc2, precision="fp32"):
     Returns int64 [N1]: the match in desc2, or -1 where not mutual."""
     a = desc1.float().contiguous()
     b = desc2.float().contiguous()
-    _, n12 = KnnIndex(b, precision).search(a, 1)
-    _, n21 = KnnIndex(a, precision).search(b, 1)
+    _, n12 = KnnIndex(b, precision).search(a, 1, verify=True)
+    _, n21 = KnnIndex(a, precision).search(b, 1, verify=True)
     return _ops.mutual_nn(n12[:, 0], n21[:, 0])

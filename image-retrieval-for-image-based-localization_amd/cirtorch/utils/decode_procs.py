@@ -126,6 +126,11 @@ class ProcDecoder:
         finally:
             sys.modules["__main__"] = main
         self._procs = list(getattr(self.pool, "_pool", []))  # the workers as started
+        # each worker's sentinel: a pipe end that becomes readable when the process ends,
+        # whoever reaps it (the Pool's maintenance thread polls exitcode concurrently, and a
+        # racing Popen.poll() can miss the exit: ECHILD -> None)
+        self._sentinels = [p.sentinel for p in self._procs]
+        self._died = False
         self.lock = threading.Lock()
         self.free = list(range(nslots))
         self.busy = []      # (event, [slots]) waiting for their H2D copy
@@ -134,7 +139,13 @@ class ProcDecoder:
     def worker_died(self):
         """True once any of the started workers has exited (multiprocessing.Pool
         replaces a dead worker but never re-runs the task it held)"""
-        return any(p.exitcode is not None for p in self._procs)
+        if not self._died and self._sentinels:
+            from multiprocessing.connection import wait
+            try:
+                self._died = bool(wait(self._sentinels, timeout=0))
+            except (OSError, ValueError):    # a sentinel already closed: its process is gone
+                self._died = True
+        return self._died
 
     def _reclaim(self, block):
         keep = []

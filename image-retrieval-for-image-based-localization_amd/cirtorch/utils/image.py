@@ -4,7 +4,8 @@
 On the extraction path this never runs: the engine's stem kernel normalises the
 pixels it loads (``rr_stem_conv_pool*``, ``rr_image_to_nhwc``).  This is the
 standalone utility for callers of the reference's name.  Statistics may be a
-scalar, one value per channel ``[C]`` or one per image and channel ``[N, C]``;
+scalar, one value per channel ``[C]`` or one per image and channel ``[N, C]``
+(the latter for ``[..., N, C, H, W]`` inputs: N is dimension -4);
 channels are dimension -3 of ``[..., C, H, W]`` (for the 4-D batches the
 reference takes, the same elements and the same two IEEE operations per element
 as its ``view(N, C, -1)`` form, so the results are bit-identical)."""
@@ -25,7 +26,7 @@ def _stat(value, data, what):
             raise ValueError("%s has %d values for %d channels (shapes %s, %s)"
                              % (what, t.shape[0], channels, tuple(t.shape), tuple(data.shape)))
         return t.reshape(channels, 1, 1)
-    if t.dim() == 2 and tuple(t.shape) == tuple(data.shape[:2]):
+    if t.dim() == 2 and data.dim() >= 4 and tuple(t.shape) == tuple(data.shape[-4:-2]):
         return t.reshape(t.shape[0], t.shape[1], 1, 1)
     raise ValueError("%s of shape %s does not match images of shape %s" % (what, tuple(t.shape), tuple(data.shape)))
 

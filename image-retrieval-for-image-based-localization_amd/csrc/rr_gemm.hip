@@ -1800,7 +1800,9 @@ static bool try_gemm8a(const ConvArgs& a, bool k1, bool perm, hipStream_t s) {
         const int tiles_p = (a.P + 255) / 256;
         const int ntiles = tiles_p;  // c_out = 128: one channel tile
         // persistent (RR_TUNE_GEMM8 value | 128: one block per tile)
-        const int grid = g_gemm8a_tile ? ntiles : std::min(ntiles, grid_cus());
+        // (a grid below 8 blocks would leave some XCD's tile range without a block)
+        const int cus = grid_cus();
+        const int grid = g_gemm8a_tile || cus < 8 || ntiles < cus ? ntiles : cus;
         if (k1) hipLaunchKernelGGL((k_gemm8a<T, 1>), dim3(grid), dim3(512), 0, s, a, tiles_p, ntiles);
         else hipLaunchKernelGGL((k_gemm8a<T, 2>), dim3(grid), dim3(512), 0, s, a, tiles_p, ntiles);
         return true;

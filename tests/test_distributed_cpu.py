@@ -26,8 +26,9 @@ def _free_port():
 class _CpuLocal:
     def __init__(self, rows, row0):
         self.rows, self.row0 = rows, row0
+        self.ntotal = rows.shape[0]
 
-    def search(self, q, k):
+    def search(self, q, k, verify=False):
         from oracle import ops
         s, i = ops.topk_exact(self.rows.numpy(), q.numpy(), k)
         if i.shape[1] < k:  # shard smaller than k: pad like the kernel (-1)
@@ -42,16 +43,20 @@ class _CpuLocalFlaky(_CpuLocal):
     flags exactly those (the certificate), so only the verified merge is exact."""
 
     def search(self, q, k, verify=False):
-        from cirtorch.search import Pending
         s, i = _CpuLocal.search(self, q, k)
         if verify is True:
             return s, i
+        return self.search_checked(q, k)[:2]
+
+    def search_checked(self, q, k):
+        """(scores, idx, uncertain flags) -- ShardedIndex's certified path"""
         unc = torch.tensor([(j + self.row0) % 3 == 0 for j in range(q.shape[0])], dtype=torch.int32)
         bad_rows = torch.nonzero(unc).flatten()
+        s, i = _CpuLocal.search(self, q, k)
         s2, i2 = _CpuLocal.search(self, q, k + 1)
         s, i = s.clone(), i.clone()
         s[bad_rows], i[bad_rows] = s2[bad_rows, 1:], i2[bad_rows, 1:]     # the best row lost
-        return s, i, Pending(unc, lambda bad: _CpuLocal.search(self, q[bad], k), s, i)
+        return s, i, unc
 
 
 def _cpu_merge(gs, gi, k):
@@ -90,7 +95,7 @@ def _worker(rank, world, port, n, d, q, k, ret, verify=False):
             s, i = idx.search(qa, k, verify=True)
             ret[rank] = (s.numpy(), i.numpy())
         else:
-            s, i = idx.search(qa, k)
+            s, i = idx.search(qa, k, verify=False)
             ret[rank] = (s.numpy(), i.numpy())
     finally:
         dist.destroy_process_group()

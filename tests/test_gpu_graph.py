@@ -42,10 +42,10 @@ def test_graphed_search_equals_eager(cuda):
     q1 = torch.from_numpy(data.unit_rows(8, 256, seed=42)).to(cuda)
     q2 = torch.from_numpy(data.unit_rows(8, 256, seed=43)).to(cuda)
     index = KnnIndex(db, "bf16")
-    g = GraphedForward(lambda q: index.search(q, 20), q1)
+    g = GraphedForward(lambda q: index.search(q, 20, verify=False), q1)
     for q in (q1, q2):
         s, i = g(q)
-        es, ei = index.search(q, 20)
+        es, ei = index.search(q, 20, verify=False)
         assert torch.equal(i, ei) and torch.equal(s, es)
         ref_s, ref_i = ops.topk_exact(db.cpu().numpy(), q.cpu().numpy(), 20)
         np.testing.assert_array_equal(i.cpu().numpy(), ref_i)

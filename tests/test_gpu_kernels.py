@@ -807,12 +807,19 @@ def test_gemm8a_bit_identical_to_tiled_engine(cuda, shape, prec):
         c = _ops().conv2d_fused(x, wp, k, k, s, 1, cout, sc, sh, leaky=True, perm32=True)
         E.check(E.lib().rr_set_tuning(8, 1 | 16), "rr_set_tuning")
         b = _ops().conv2d_fused(x, wp, k, k, s, 1, cout, sc, sh, leaky=True, perm32=True)
+        # a grid capped below the 8 XCDs (RR_TUNE_GRID_CUS = 4): one block per tile then
+        # (the persistent grid left XCDs 4..7's tile ranges unwritten)
+        E.check(E.lib().rr_set_tuning(8, 1), "rr_set_tuning")
+        E.check(E.lib().rr_set_tuning(7, 4), "rr_set_tuning")
+        d = _ops().conv2d_fused(x, wp, k, k, s, 1, cout, sc, sh, leaky=True, perm32=True)
     finally:
+        E.lib().rr_set_tuning(7, 0)
         E.lib().rr_set_tuning(8, 1)
         E.lib().rr_set_tuning(6, 1)
         E.lib().rr_set_tuning(5, 1)
     assert torch.equal(a, b)
     assert torch.equal(a, c)
+    assert torch.equal(a, d)
     ref = F.conv2d(x[:1].cpu().permute(0, 3, 1, 2).double(), wt.to(dt).cpu().double(), stride=s, padding=1)
     ref = ref * sc.cpu().double()[None, :, None, None] + sh.cpu().double()[None, :, None, None]
     ref = F.leaky_relu(ref, 0.01).permute(0, 2, 3, 1)

@@ -146,7 +146,7 @@ def test_fp16_screening_copy_and_limits(cuda):
 @pytest.mark.parametrize("prec", ["bf16", "int8"])
 def test_knn_full_size_1m_bench_shape(cuda, prec):
     """BASELINE config size (1M x 2048 database, 128 queries, k = 100, bf16 or
-    int8 screening) through size-independent properties: a query that is a database
+    int8 screening, the uncertified screen) through size-independent properties: a query that is a database
     row retrieves itself first with score 1; two queries checked against the
     CPU oracle over the whole database (chunked exact float64 top-k); a
     4-shard search + merge is bit-identical to the single search."""
@@ -159,7 +159,7 @@ def test_knn_full_size_1m_bench_shape(cuda, prec):
     self_rows = [5, 77777, 500000, n - 1]
     qq[:4] = db[self_rows]
     index = KnnIndex(db, prec)
-    s, i = index.search(qq, k)
+    s, i = index.search(qq, k, verify=False)   # the raw screen; the certified mode: next test
     i_np, s_np = i.cpu().numpy(), s.cpu().numpy()
     assert i_np[:4, 0].tolist() == self_rows
     assert np.abs(s_np[:4, 0] - 1.0).max() < 1e-6
@@ -180,11 +180,83 @@ def test_knn_full_size_1m_bench_shape(cuda, prec):
     R, per = 4, n // 4
     ss, ii = [], []
     for r in range(R):
-        sh_s, sh_i = KnnIndex(db[r * per:(r + 1) * per], prec, idx_offset=r * per).search(qq, k)
+        sh_s, sh_i = KnnIndex(db[r * per:(r + 1) * per], prec, idx_offset=r * per).search(qq, k, verify=False)
         ss.append(sh_s)
         ii.append(sh_i)
     sm, im = merge_topk(torch.stack(ss), torch.stack(ii), k)
     assert torch.equal(im, i) and torch.equal(sm, s)
+
+
+def _exact_topk_1m(db, q_np, k, chunk=125_000):
+    """the exact (float64 score desc, index asc) top-k of a few queries over a
+    device database, chunk by chunk on the host (oracle ops.topk_exact)"""
+    from oracle import ops
+    cs, ci = [], []
+    for r0 in range(0, db.shape[0], chunk):
+        s_c, i_c = ops.topk_exact(db[r0:r0 + chunk].cpu().numpy(), q_np, k)
+        cs.append(s_c)
+        ci.append(i_c + r0)
+    cs, ci = np.concatenate(cs, 1), np.concatenate(ci, 1)
+    out_s, out_i = [], []
+    for j in range(q_np.shape[0]):
+        order = np.lexsort((ci[j], -cs[j]))[:k]
+        out_s.append(cs[j][order])
+        out_i.append(ci[j][order])
+    return np.stack(out_s), np.stack(out_i)
+
+
+def test_knn_headline_fp16_deferred_q1024(cuda):
+    """The bench's headline search mode at its own shape (bench.py run_steps / match):
+    1M x 2048 database, Q = 1024 queries per search, k = 100, fp16 screening with the
+    deferred certificate, the next batch's search queued before the previous one is
+    resolved.  Six queries sit on planted 2048-d near-duplicate clusters (600 rows at
+    noise 0.01: scores within ~2e-4 of each other, under the fp16 error bound ~1e-3), so
+    the certificate must fire at D = 2048 and the repair run (requeried > 0).  Checks:
+    every query bit-identical (indices and float64 scores) to an fp32-screened
+    verify=True search; the planted queries + 6 random ones + 2 self-retrievals equal
+    the chunked exact host oracle over all 1M rows; the flagged set covers the planted
+    queries.  Reference: scripts/test.py:247-248 (np.dot + np.argsort)."""
+    from cirtorch import _ops
+    from cirtorch.search import KnnIndex
+    n, d, q, k = 1_000_000, 2048, 1024, 100
+    db = _ops.fill_unit_rows(n, d, seed=0xDB5EED, device=cuda)
+    qa = _ops.fill_unit_rows(q, d, seed=0x0E5EED, device=cuda)
+    qb = _ops.fill_unit_rows(q, d, seed=0x0E5EEE, device=cuda)
+    gen = torch.Generator(device=cuda).manual_seed(77)
+    planted = [3, 200, 511, 512, 800, 1023]          # queries of batch a with a cluster
+    for c, j in enumerate(planted):
+        rows = qa[j] + 0.01 * torch.randn((600, d), generator=gen, device=cuda)
+        r0 = 1000 + c * 160_000                      # one cluster per region of the database
+        db[r0:r0 + 600] = rows / rows.norm(dim=1, keepdim=True)
+    self_rows = [7, 999_999]
+    qa[[40, 41]] = db[self_rows]
+    index = KnnIndex(db, "fp16")
+    # the bench's order: search a, search b, resolve a, resolve b
+    sa, ia, pa = index.search(qa, k, verify="deferred")
+    sb, ib, pb = index.search(qb, k, verify="deferred")
+    na, nb = pa.resolve(), pb.resolve()
+    assert na >= len(planted), na                    # the certificate fired at D = 2048
+    assert nb == 0, nb                               # random queries certify
+    _, _, unc = index.search_checked(qa, k)
+    flagged = set(torch.nonzero(unc).flatten().tolist())
+    assert set(planted) <= flagged, (planted, sorted(flagged))
+    # every query == the fp32-screened certified search, bit for bit
+    ref = KnnIndex(db, "fp32")
+    for (s, i, qq) in ((sa, ia, qa), (sb, ib, qb)):
+        s32, i32 = ref.search(qq, k, verify=True)
+        assert torch.equal(i, i32) and torch.equal(s, s32)
+    del ref
+    torch.cuda.empty_cache()
+    # 14 queries against the exact host oracle over all 1M rows
+    pick = planted + [0, 1, 2, 300, 600, 900] + [40, 41]
+    ref_s, ref_i = _exact_topk_1m(db, qa[pick].cpu().numpy(), k)
+    np.testing.assert_array_equal(ia[pick].cpu().numpy(), ref_i)
+    np.testing.assert_allclose(sa[pick].cpu().numpy(), ref_s, rtol=0, atol=1e-12)
+    assert ia[40, 0].item() == self_rows[0] and ia[41, 0].item() == self_rows[1]
+    # the planted clusters are what the planted queries retrieve
+    for c, j in enumerate(planted):
+        r0 = 1000 + c * 160_000
+        assert ((ia[j] >= r0) & (ia[j] < r0 + 600)).all()
 
 
 def _fused_vs_slab(cuda, db, qq, k, prec):
@@ -194,10 +266,10 @@ def _fused_vs_slab(cuda, db, qq, k, prec):
     from cirtorch.search import KnnIndex
     index = KnnIndex(torch.from_numpy(db).to(cuda), prec)
     q = torch.from_numpy(qq).to(cuda)
-    s1, i1 = index.search(q, k)
+    s1, i1 = index.search(q, k, verify=False)
     E.check(E.lib().rr_set_tuning(9, 0), "rr_set_tuning")
     try:
-        s0, i0 = index.search(q, k)
+        s0, i0 = index.search(q, k, verify=False)
     finally:
         E.lib().rr_set_tuning(9, 1)
     return (s1.cpu().numpy(), i1.cpu().numpy()), (s0.cpu().numpy(), i0.cpu().numpy())
@@ -333,13 +405,13 @@ def test_knn_fused_graph_replay(cuda):
     q1 = torch.from_numpy(data.unit_rows(300, 256, seed=72)).to(cuda)
     q2 = torch.from_numpy(data.unit_rows(300, 256, seed=73)).to(cuda)
     index = KnnIndex(db, "bf16")
-    g = GraphedForward(lambda q: index.search(q, 50), q1)
+    g = GraphedForward(lambda q: index.search(q, 50, verify=False), q1)
     for q in (q1, q2, q1):
         s, i = g(q)
-        es, ei = index.search(q, 50)
+        es, ei = index.search(q, 50, verify=False)
         assert torch.equal(i, ei) and torch.equal(s, es)
     ref_s, ref_i = ops.topk_exact(db.cpu().numpy(), q2.cpu().numpy(), 50)
-    np.testing.assert_array_equal(index.search(q2, 50)[1].cpu().numpy(), ref_i)
+    np.testing.assert_array_equal(index.search(q2, 50, verify=False)[1].cpu().numpy(), ref_i)
 
 
 @pytest.mark.parametrize("prec", ["bf16", "fp16", "fp32", "int8"])
@@ -391,7 +463,7 @@ def test_knn_half_width_gemm_equals_tiled(cuda, prec, nq):
     try:
         for v in (1, 9):
             E.check(E.lib().rr_set_tuning(8, v), "rr_set_tuning")
-            out[v] = KnnIndex(db, prec).search(q, 100)
+            out[v] = KnnIndex(db, prec).search(q, 100, verify=False)
     finally:
         E.lib().rr_set_tuning(8, 1)
     assert torch.equal(out[1][1], out[9][1])
@@ -416,11 +488,11 @@ def test_int8_quantization_and_score_gemm(cuda):
     db_np = db.cpu().numpy()
     for nq in (100, 1024):
         qq = _ops.fill_unit_rows(nq, 2048, seed=0x5EEDB + nq, device=cuda)
-        s, i = index.search(qq, 100)
+        s, i = index.search(qq, 100, verify=False)
         ref_s, ref_i = ops.topk_exact(db_np, qq[:6].cpu().numpy(), 100)
         np.testing.assert_array_equal(i[:6].cpu().numpy(), ref_i)
         np.testing.assert_allclose(s[:6].cpu().numpy(), ref_s, rtol=0, atol=1e-12)
-        s2, i2 = KnnIndex(db, "bf16").search(qq, 100)
+        s2, i2 = KnnIndex(db, "bf16").search(qq, 100, verify=False)
         assert torch.equal(i, i2) and torch.equal(s, s2)
 
 
@@ -436,7 +508,7 @@ def test_knn_rescore_cut_changes_nothing(cuda, prec):
     db = _ops.fill_unit_rows(300_000, 512, seed=0xC0FE, device=cuda)
     q = _ops.fill_unit_rows(200, 512, seed=0xC0FF, device=cuda)
     index = KnnIndex(db, prec)
-    s0, i0 = index.search(q, 100)                       # unchecked: every candidate re-scored
+    s0, i0 = index.search(q, 100, verify=False)         # unchecked: every candidate re-scored
     s1, i1, unc = index.search_checked(q, 100)          # checked: the cut
     assert torch.equal(i0, i1) and torch.equal(s0, s1)
     assert int(unc.sum()) == 0

@@ -52,6 +52,16 @@ def test_normalize_errors():
         normalize(x.numpy(), [0.1, 0.2, 0.3], [1.0, 1.0, 1.0])
     with pytest.raises(TypeError):
         normalize(x, "mean", [1.0, 1.0, 1.0])
+    # [N, C] statistics index dims -4 / -3: a 5-D [B, N, C, H, W] batch takes [N, C] stats,
+    # a stat shaped like the leading (B, N) dims is refused
+    x5 = torch.rand((2, 4, 3, 5, 5))
+    m5 = torch.rand((4, 3))
+    got = normalize(x5, m5, torch.ones(4, 3))
+    assert torch.equal(got, x5 - m5[:, :, None, None])
+    with pytest.raises(ValueError):
+        normalize(x5, torch.rand((2, 4)), torch.ones(2, 4))
+    with pytest.raises(ValueError):
+        normalize(torch.rand((3, 5, 5)), torch.rand((1, 3)), torch.ones(1, 3))
 
 
 def test_host_half_under_asan():

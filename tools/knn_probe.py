@@ -32,7 +32,7 @@ def main():
     def one():
         if args.verify:
             return idx.search(q, 100, verify="deferred")[2]
-        idx.search(q, 100)
+        idx.search(q, 100, verify=False)
         return None
     p = one()
     if p is not None:
