@@ -663,6 +663,194 @@ __global__ void __launch_bounds__(512, 1) k_pair_mid(PairMidArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// The same boundary with a deeper HBM stream (round 6, the default; RR_TUNE_PAIR_MID = 0 runs
+// k_pair_mid above).  k_pair_mid's 64-pixel tiles leave one residual tile (64 KiB) in flight
+// per CU, issued at the tile start and landed long before the tile ends, and its x tile
+// is issued after stage 1, so the next tile's wait also drains the y stores: the read
+// stream idles for part of every tile (4.6 TB/s of algorithmic traffic in the bench step).
+// Here tiles are TP = 32 pixels, the residual tiles sit in a 4-slot ring (3 tiles ahead: up
+// to 96 KiB of reads in flight per CU) and x is double buffered (one tile ahead), both
+// issued at the top of the tile, before its stores: the counted wait at the next top covers
+// only the loads it needs, never the stores.  Per tile (iteration k, tile t_k):
+//   top: vmcnt(10) = x(t_k) and r(t_k) have landed (younger: r(t_{k+2}) 4, y(t_{k-1}) 4,
+//        z(t_{k-1}) 2 per lane), barrier; issue x(t_{k+1}) (1 per lane), r(t_{k+3}) (4);
+//   stage 1 / barrier / stage 2 as in k_pair_mid on 32 pixels (same fragments and K order
+//   per element: bit-identical).
+// DMAs of tiles past the end are issued anyway (their offsets read past the buffer: zeros),
+// so every lane's count is the same on every tile.
+template <typename H>
+__global__ void __launch_bounds__(512, 1) k_pair_mid_ring(PairMidArgs a) {
+    constexpr int K3 = 128, C3 = 512, C1 = 128, TP = 32, NR = 4;
+    constexpr int XB = TP * K3 * 2, RB = TP * C3 * 2;  // 8 KiB, 32 KiB
+    __shared__ __attribute__((aligned(1024))) char smem[NR * RB + 2 * XB];
+    __shared__ __attribute__((aligned(16))) float sS3[C3], sH3[C3], sS1[C1], sH1[C1];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r16 = lane & 15, kq = lane >> 4;
+    for (int i = tid; i < C3; i += 512) {
+        sS3[i] = a.s3[i];
+        sH3[i] = a.h3[i];
+    }
+    if (tid < C1) {
+        sS1[tid] = a.s1[tid];
+        sH1[tid] = a.h1[tid];
+    }
+    uint4 a3[4][4], a1[16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+            a3[i][kk] = *reinterpret_cast<const uint4*>(a.w3 + (long long)(64 * wave + 16 * i + r16) * K3 + 32 * kk + 8 * kq);
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk)
+        a1[kk] = *reinterpret_cast<const uint4*>(a.w1 + (long long)(16 * wave + r16) * C3 + 32 * kk + 8 * kq);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) pin_loaded(a3[i][kk]);
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) pin_loaded(a1[kk]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the weights: the counted waits below see only DMA / stores
+    __syncthreads();
+
+    const long long P = a.P;
+    const int ntiles = (int)((P + TP - 1) / TP);
+    const int t0 = (int)blockIdx.x, G = (int)gridDim.x;
+    if (t0 >= ntiles) return;
+    const si32x4_t rsX = srsrc(a.x, (unsigned)(P * K3 * 2));
+    const si32x4_t rsR = srsrc(a.res, (unsigned)(P * C3 * 2));
+    const unsigned lds0 = (unsigned)(unsigned long long)smem;
+    const unsigned ldsX = lds0 + NR * RB;
+    // x tile: 8 wave-instructions of 4 pixels x 256 B (one per wave)
+    auto dma_x = [&](int t, int xb) {
+        const int px = 4 * wave + (lane >> 4), slot = lane & 15;
+        const unsigned off = (unsigned)(((long long)t * TP + px) * (K3 * 2)) + (unsigned)((slot ^ (px & 15)) << 4);
+        sdma16(rsX, off, ldsX + xb * XB + wave * 1024);
+    };
+    // residual tile: 32 wave-instructions of one pixel x 1 KiB (4 per wave)
+    auto dma_r = [&](int t, int buf) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int px = 4 * wave + u;
+            const unsigned off = (unsigned)(((long long)t * TP + px) * (C3 * 2)) + (unsigned)((lane ^ (px & 15)) << 4);
+            sdma16(rsR, off, lds0 + buf * RB + px * 1024);
+        }
+    };
+    const bool leaky3 = a.act3 == RR_ACT_LEAKY, leaky1 = a.act1 == RR_ACT_LEAKY;
+
+    dma_x(t0, 0);
+    dma_r(t0, 0);
+    dma_r(t0 + G, 1);
+    dma_r(t0 + 2 * G, 2);
+    for (int k = 0, t = t0; t < ntiles; ++k, t += G) {
+        const int cur = k & 3, xc = k & 1;
+        if (k == 0) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(10)\n\ts_barrier" ::: "memory");
+        dma_x(t + G, xc ^ 1);
+        dma_r(t + 3 * G, (k + 3) & 3);
+        const char* X = smem + NR * RB + xc * XB;
+        char* RY = smem + cur * RB;
+        // ---- stage 1: y = act3(W3 x * s3 + h3 + r), one 32-channel pair at a time
+#pragma unroll
+        for (int i2 = 0; i2 < 2; ++i2) {
+            h16_f32x4_t acc[2][2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[h][j] = (h16_f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                uint4 bx[2];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int px = 16 * j + r16;
+                    bx[j] = *reinterpret_cast<const uint4*>(X + px * (K3 * 2) + ((((4 * kk + kq) ^ (px & 15))) << 4));
+                }
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) acc[h][j] = H16<H>::mfma(a3[2 * i2 + h][kk], bx[j], acc[h][j]);
+            }
+            const int c = 64 * wave + 32 * i2 + 8 * kq;  // 8 consecutive channels of this lane (PERM32)
+            const int chunk = c >> 3;
+            const float4 sc0 = *reinterpret_cast<const float4*>(sS3 + c);
+            const float4 sc1 = *reinterpret_cast<const float4*>(sS3 + c + 4);
+            const float4 sh0 = *reinterpret_cast<const float4*>(sH3 + c);
+            const float4 sh1 = *reinterpret_cast<const float4*>(sH3 + c + 4);
+            const float sc[8] = {sc0.x, sc0.y, sc0.z, sc0.w, sc1.x, sc1.y, sc1.z, sc1.w};
+            const float sh[8] = {sh0.x, sh0.y, sh0.z, sh0.w, sh1.x, sh1.y, sh1.z, sh1.w};
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int px = 16 * j + r16;
+                uint4* slot = reinterpret_cast<uint4*>(RY + px * (C3 * 2) + ((chunk ^ (px & 15)) << 4));
+                const uint4 q = *slot;
+                const unsigned w4[4] = {q.x, q.y, q.z, q.w};
+                float v[8];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    v[r] = acc[0][j][r] * sc[r] + sh[r];
+                    v[4 + r] = acc[1][j][r] * sc[4 + r] + sh[4 + r];
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    v[2 * r] += H16<H>::lo(w4[r]);
+                    v[2 * r + 1] += H16<H>::hi(w4[r]);
+                }
+                if (leaky3) {
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * a.slope3;
+                }
+                uint4 o;
+                o.x = H16<H>::pack2(v[0], v[1]);
+                o.y = H16<H>::pack2(v[2], v[3]);
+                o.z = H16<H>::pack2(v[4], v[5]);
+                o.w = H16<H>::pack2(v[6], v[7]);
+                *slot = o;
+                const long long p = (long long)t * TP + px;
+                if (p < P) st16_once(a.y + p * C3 + c, o);
+            }
+        }
+        // y tile complete in LDS; the x buffer of this tile is free
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        // ---- stage 2: z = act1(W1 y * s1 + h1), K = 512 from the LDS y tile
+        h16_f32x4_t zacc[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) zacc[j] = (h16_f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk) {
+            uint4 by[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int px = 16 * j + r16;
+                by[j] = *reinterpret_cast<const uint4*>(RY + px * (C3 * 2) + ((((4 * kk + kq) ^ (px & 15))) << 4));
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) zacc[j] = H16<H>::mfma(a1[kk], by[j], zacc[j]);
+        }
+        {
+            const int c = 32 * (wave >> 1) + 8 * kq + 4 * (wave & 1);
+            const float4 sc = *reinterpret_cast<const float4*>(sS1 + c);
+            const float4 sh = *reinterpret_cast<const float4*>(sH1 + c);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                float v[4] = {zacc[j][0] * sc.x + sh.x, zacc[j][1] * sc.y + sh.y, zacc[j][2] * sc.z + sh.z,
+                              zacc[j][3] * sc.w + sh.w};
+                if (leaky1) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * a.slope1;
+                }
+                uint2 o;
+                o.x = H16<H>::pack2(v[0], v[1]);
+                o.y = H16<H>::pack2(v[2], v[3]);
+                const long long p = (long long)t * TP + 16 * j + r16;
+                if (p < P) st8_once(a.z + p * C1 + c, o);
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 
 // ---------------------------------------------------------------------------
 // Weight-stationary 1x1 with the weights in VGPRs (the bottleneck conv3 of
@@ -882,6 +1070,7 @@ void launch_s_t(const ConvArgs& a, hipStream_t s) {
 
 int g_stream_mode = 1;  // rr_set_tuning(RR_TUNE_STREAM_1X1): 0 off, 1 auto, 2 / 3 see launch_stream1x1
 int g_wres = 2;         // rr_set_tuning(RR_TUNE_WRES)
+int g_pair_mid = 1;     // rr_set_tuning(RR_TUNE_PAIR_MID): 1 k_pair_mid_ring (default), 0 k_pair_mid
 
 namespace {
 template <int K, int CW>
@@ -1022,10 +1211,15 @@ extern "C" int rr_conv1x1_pair(const void* x, long long p, int c_in, const void*
             m.res = (const bf16_t*)residual + p0 * 512; m.w1 = (const bf16_t*)w1; m.s1 = scale1; m.h1 = shift1;
             m.y = (bf16_t*)y + p0 * 512; m.z = (bf16_t*)z + p0 * 128; m.P = pn;
             m.act3 = act3; m.act1 = act1; m.slope3 = slope3; m.slope1 = slope1;
-            const long long ntiles = (pn + 63) / 64;
+            const long long ntiles = (pn + (g_pair_mid ? 31 : 63)) / (g_pair_mid ? 32 : 64);
             const int grid = (int)(ntiles < g_pair_cus ? ntiles : g_pair_cus);
-            if (dtype == RR_F16) hipLaunchKernelGGL(k_pair_mid<f16_t>, dim3(grid), dim3(512), 0, s, m);
-            else hipLaunchKernelGGL(k_pair_mid<bf16_t>, dim3(grid), dim3(512), 0, s, m);
+            if (g_pair_mid) {
+                if (dtype == RR_F16) hipLaunchKernelGGL(k_pair_mid_ring<f16_t>, dim3(grid), dim3(512), 0, s, m);
+                else hipLaunchKernelGGL(k_pair_mid_ring<bf16_t>, dim3(grid), dim3(512), 0, s, m);
+            } else {
+                if (dtype == RR_F16) hipLaunchKernelGGL(k_pair_mid<f16_t>, dim3(grid), dim3(512), 0, s, m);
+                else hipLaunchKernelGGL(k_pair_mid<bf16_t>, dim3(grid), dim3(512), 0, s, m);
+            }
         }
         return check_launch("rr_conv1x1_pair");
     }

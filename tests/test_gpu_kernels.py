@@ -457,7 +457,7 @@ def test_stem_pool_before_epilogue_bit_identical(cuda, dt, shape):
     xu = (x * 255).to(torch.uint8)
     outs = {}
     try:
-        for mode in (0, 1, 2, 3, 4):
+        for mode in (0, 1, 2, 3, 4, 6):
             E.check(E.lib().rr_set_tuning(11, mode), "rr_set_tuning")
             outs[mode] = [ops.stem_conv_pool(inp.to(cuda), wpk, scale.to(cuda), shift.to(cuda), leaky=True,
                                              slope=0.01, mean=mean, std=std).float().cpu() for inp in (x, xu)]
@@ -473,8 +473,8 @@ def test_stem_pool_before_epilogue_bit_identical(cuda, dt, shape):
     # v3 (swapped MFMA operands, lane-local pooling, byte table for uint8) == v2
     for b, c in zip(outs[1], outs[2]):
         assert torch.equal(b, c), (b - c).abs().max().item()
-    # v3's patch fill in 2 / 5 parts (the default: 3)
-    for m in (3, 4):
+    # v3's patch fill in 2 / 5 parts (the default: 3); mode 6: v3 with the interior fast fill
+    for m in (3, 4, 6):
         for b, c in zip(outs[2], outs[m]):
             assert torch.equal(b, c), (m, (b - c).abs().max().item())
 
@@ -575,6 +575,26 @@ def test_conv1x1_pair_mod3_pixel_chunks(cuda):
     assert y.shape[1] * y.shape[2] > (1 << 20)
     assert torch.equal(y, y2)
     assert torch.equal(z, z2)
+
+
+@pytest.mark.parametrize("shape", [(1, 3, 7), (2, 23, 37), (3, 96, 128), (1, 1031, 1029)])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_conv1x1_pair_mod3_ring_equals_64px_kernel(cuda, dt, shape):
+    """RR_TUNE_PAIR_MID: the 128/512 boundary on 32-pixel tiles with the 4-slot residual
+    ring (default, k_pair_mid_ring) vs the 64-pixel one-ahead kernel (k_pair_mid): y and z
+    bit for bit -- fewer pixels than one tile, a partial last tile, several tiles per block,
+    more than 2^20 pixels (two chunk launches)."""
+    from cirtorch import _engine as E
+    n, h, w = shape
+    try:
+        E.check(E.lib().rr_set_tuning(15, 0), "rr_set_tuning")
+        y0, z0, _, _ = _mod3_pair_case(dt, n, h, w, 3 * h + w, cuda, ref=False)
+        E.check(E.lib().rr_set_tuning(15, 1), "rr_set_tuning")
+        y1, z1, _, _ = _mod3_pair_case(dt, n, h, w, 3 * h + w, cuda, ref=False)
+    finally:
+        E.lib().rr_set_tuning(15, 1)
+    assert torch.equal(y0, y1)
+    assert torch.equal(z0, z1)
 
 
 @pytest.mark.parametrize("c_out", [64, 128])
