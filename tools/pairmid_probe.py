@@ -55,7 +55,7 @@ def main():
     for mode in (0, 1):
         best = min(t[mode])
         print("pair_mid mode %d (%s): %s us, best %.1f us = %.2f TB/s algorithmic" % (
-            mode, "ring 32 px" if mode else "64 px", " ".join("%.1f" % v for v in t[mode]), best, gb / best * 1e3 / 1e3))
+            mode, "ring 32 px" if mode else "64 px", " ".join("%.1f" % v for v in t[mode]), best, gb / best * 1e3))
     print("bit-identical:", same)
 
 
