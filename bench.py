@@ -1134,7 +1134,7 @@ def main():
                      "frac": achieved / peak, "traffic": traffic, "traffic_note": traffic_note,
                      "algorithmic_bytes": bytes_img * B,
                      "note": "dominant kernel family = the extractor body's 53 conv layers per forward (k_stem_pool3, "
-                             "k_gemm8 / k_gemm8a, k_c3s_w128, k_c3w64 / k_conv3x3, k_wres1x1 / k_stream1x1, fused boundaries k_stream_pair / k_pair_mid, "
+                             "k_gemm8 / k_gemm8a, k_c3s_w128, k_c3w64 / k_conv3x3, k_wres1x1 / k_stream1x1, fused boundaries k_c3pair / k_pair_mid_ring, "
                              "k_igemm; "
                              "their per-kernel rocprof averages sum to this time, see profiles/); algorithmic_bytes = "
                              "per-layer unfused input + output (+ residual) bytes, so the fused boundaries can bring "
@@ -1178,6 +1178,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:
+        out["build"] = out.pop("build")  # last: inside the tail of stdout a driver keeps
         print(json.dumps(out))
     if world > 1:
         dist.barrier()
