@@ -308,6 +308,7 @@ extern int g_stream_xcd;
 extern int g_conv3s;
 extern int g_wres;
 extern int g_pair_mid;
+extern int g_wres_ring;
 
 // out[R][k] = w[chan(R)][ci][kh][kw] with k = (kh*KW + kw)*cin_pad + ci, zeros elsewhere.
 template <typename T>
@@ -446,7 +447,7 @@ namespace rr {
 void set_gemm_tuning(int key, int value);
 }
 extern "C" int rr_set_tuning(int key, int value) {
-    if (key < 0 || key > 15) return fail(RR_EINVAL, "rr_set_tuning: unknown key");
+    if (key < 0 || key > 16) return fail(RR_EINVAL, "rr_set_tuning: unknown key");
     if (key == RR_TUNE_KNN_FUSED) {
         rr::g_knn_fused = value != 0;
         return RR_OK;
@@ -464,6 +465,7 @@ extern "C" int rr_set_tuning(int key, int value) {
     else if (key == RR_TUNE_CONV3S) rr::g_conv3s = value;
     else if (key == RR_TUNE_WRES) rr::g_wres = value;
     else if (key == RR_TUNE_PAIR_MID) rr::g_pair_mid = value;
+    else if (key == RR_TUNE_WRES_RING) rr::g_wres_ring = value;
     else rr::set_gemm_tuning(key, value);
     return RR_OK;
 }

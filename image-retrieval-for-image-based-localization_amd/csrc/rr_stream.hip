@@ -888,12 +888,15 @@ struct WresArgs {
     int h, w_, ho, wo, stride;
 };
 
-template <int K, int CW, bool RES, typename H>
+template <int K, int CW, bool RES, typename H, bool DEEP = true>
 __global__ void __launch_bounds__(512, 1) k_wres1x1(WresArgs a) {
     constexpr int TP = 32, NJ = TP / 16, NI = CW / 16, NK = K / 32, BC = 8 * CW;
     constexpr int XRB = K * 2, RRB = RES ? BC * 2 : 0;  // row bytes of the two tiles
     constexpr int XB = TP * XRB, RB = TP * RRB;         // tile bytes
-    constexpr int BUF = XB + RB, NBUF = 3;
+    // buffers: 3 (two tiles ahead) where the residual tile fills the LDS; the non-residual forms
+    // (16 / 32 KiB tiles) keep 5 / 3 tiles ahead (round 6: the strided mod3 projection streamed
+    // at 4.7 TB/s two tiles ahead)
+    constexpr int BUF = XB + RB, NBUF = RES || !DEEP ? 3 : (BUF <= 16384 ? 6 : 4), DA = NBUF - 1;
     constexpr int NDX = XB / 1024 / 8, NDR = RB / 1024 / 8;  // DMA instructions per wave
     constexpr int ND = NDX + NDR, NST = (CW / 32) * NJ;      // ... and stores per wave per tile
     static_assert(NI * NK <= 32 && XB % 8192 == 0 && RB % 8192 == 0, "tile shape");
@@ -963,21 +966,37 @@ __global__ void __launch_bounds__(512, 1) k_wres1x1(WresArgs a) {
     };
     const bool leaky = a.act == RR_ACT_LEAKY;
 
-    dma(bi, 0);
-    if (bi + G < ntiles) dma(bi + G, 1);
+    if constexpr (DA == 2) {
+        dma(bi, 0);
+        if (bi + G < ntiles) dma(bi + G, 1);
+    } else {
+        // DA tiles ahead, issued whether or not they exist (past the end: offsets past the
+        // buffers, zeros), so every wave's vmcnt count is the same on every tile
+#pragma unroll
+        for (int j = 0; j < DA; ++j) dma(bi + j * G, j);
+    }
     for (int k = 0, t = bi; t < ntiles; ++k, t += G) {
         const int cur = k % NBUF;
-        // tile t's DMA landed: still in flight after it may be tile t + G's DMA and
-        // (k > 0) this wave's stores of tile t - G, issued in that order
-        if (t + G < ntiles) {
-            if (k == 0) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(ND) : "memory");
-            else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(ND + NST) : "memory");
+        if constexpr (DA == 2) {
+            // tile t's DMA landed: still in flight after it may be tile t + G's DMA and
+            // (k > 0) this wave's stores of tile t - G, issued in that order
+            if (t + G < ntiles) {
+                if (k == 0) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(ND) : "memory");
+                else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(ND + NST) : "memory");
+            } else {
+                if (k == 0) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(NST) : "memory");
+            }
+            // every wave is past tile t - G: its buffer takes tile t + 2G
+            if (t + 2 * G < ntiles) dma(t + 2 * G, (k + 2) % NBUF);
         } else {
-            if (k == 0) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(NST) : "memory");
+            // tile t's DMA landed: younger are tiles t + G .. t + (DA - 1) G and (k > 0) the
+            // stores of tile t - G (older stores are waited for too: an over-wait, safe)
+            if (k == 0) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((DA - 1) * ND) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((DA - 1) * ND + NST) : "memory");
+            // every wave is past tile t - G: its buffer takes tile t + DA G
+            dma(t + DA * G, (k + DA) % NBUF);
         }
-        // every wave is past tile t - G: its buffer takes tile t + 2G
-        if (t + 2 * G < ntiles) dma(t + 2 * G, (k + 2) % NBUF);
         const char* X = smem + cur * BUF;
         const char* Rt = X + XB;
         h16_f32x4_t acc[NI][NJ];
@@ -1071,6 +1090,7 @@ void launch_s_t(const ConvArgs& a, hipStream_t s) {
 int g_stream_mode = 1;  // rr_set_tuning(RR_TUNE_STREAM_1X1): 0 off, 1 auto, 2 / 3 see launch_stream1x1
 int g_wres = 2;         // rr_set_tuning(RR_TUNE_WRES)
 int g_pair_mid = 1;     // rr_set_tuning(RR_TUNE_PAIR_MID): 1 k_pair_mid_ring (default), 0 k_pair_mid
+int g_wres_ring = 1;    // rr_set_tuning(RR_TUNE_WRES_RING): 1 deep rings for the non-residual k_wres1x1, 0 two ahead
 
 namespace {
 template <int K, int CW>
@@ -1107,7 +1127,8 @@ void launch_wres(const ConvArgs& a, hipStream_t s, bool f16) {
         auto go = [&](auto h) {
             using H = decltype(h);
             if (res) hipLaunchKernelGGL((k_wres1x1<K, CW, true, H>), dim3(grid), dim3(512), 0, s, w);
-            else hipLaunchKernelGGL((k_wres1x1<K, CW, false, H>), dim3(grid), dim3(512), 0, s, w);
+            else if (g_wres_ring) hipLaunchKernelGGL((k_wres1x1<K, CW, false, H>), dim3(grid), dim3(512), 0, s, w);
+            else hipLaunchKernelGGL((k_wres1x1<K, CW, false, H, false>), dim3(grid), dim3(512), 0, s, w);
         };
         if (f16) go(f16_t{});
         else go(bf16_t{});

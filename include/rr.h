@@ -388,13 +388,16 @@ int rr_rank_full(const float* db_f32, long long n, const float* q_f32, int nq, i
  *                        default); 0: the streaming 1x1 / 8-phase GEMM
  *   RR_TUNE_PAIR_MID     1 (default): the 128/512 boundary of rr_conv1x1_pair on 32-pixel tiles
  *                        with a 4-slot residual ring (3 tiles ahead); 0: 64-pixel tiles, one ahead
+ *                        (same results bit for bit)
+ *   RR_TUNE_WRES_RING    1 (default): the non-residual k_wres1x1 forms (projections, mod4 block-1
+ *                        conv1) keep 5 (K = 256) / 3 (K = 512) activation tiles in flight; 0: two
  *                        (same results bit for bit) */
 enum rr_tune_key { RR_TUNE_GEMM_CONFIG = 0, RR_TUNE_GEMM_STAGES = 1, RR_TUNE_GEMM_WIDE = 2,
                    RR_TUNE_GEMM_ASTAT = 3, RR_TUNE_GEMM_XCD_MAP = 4, RR_TUNE_STREAM_1X1 = 5,
                    RR_TUNE_CONV3X3 = 6, RR_TUNE_GRID_CUS = 7, RR_TUNE_GEMM8 = 8,
                    RR_TUNE_KNN_FUSED = 9, RR_TUNE_CONV3_PIPE = 10,
                    RR_TUNE_STEM = 11, RR_TUNE_STREAM_XCD = 12, RR_TUNE_CONV3S = 13,
-                   RR_TUNE_WRES = 14, RR_TUNE_PAIR_MID = 15 };
+                   RR_TUNE_WRES = 14, RR_TUNE_PAIR_MID = 15, RR_TUNE_WRES_RING = 16 };
 int rr_set_tuning(int key, int value);
 
 /* ----------------------------------------------------------- data helpers */

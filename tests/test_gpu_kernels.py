@@ -159,9 +159,15 @@ def test_wres1x1(cuda, case, prec):
         for on in (2, 0):
             E.check(E.lib().rr_set_tuning(14, on), "rr_set_tuning")
             outs.append(_check_conv(cuda, case, prec, True))
+        # RR_TUNE_WRES_RING = 0: the non-residual forms two tiles ahead instead of 5 / 3
+        E.check(E.lib().rr_set_tuning(14, 2), "rr_set_tuning")
+        E.check(E.lib().rr_set_tuning(16, 0), "rr_set_tuning")
+        outs.append(_check_conv(cuda, case, prec, True))
     finally:
         E.lib().rr_set_tuning(14, 2)
+        E.lib().rr_set_tuning(16, 1)
     assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[0], outs[2])
 
 
 C3W64_CASES = [
