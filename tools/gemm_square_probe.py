@@ -25,10 +25,15 @@ def timed(fn, iters=10):
 
 def main():
     from cirtorch import _ops as ops
+    from cirtorch import _engine as E
+    if os.environ.get("G8"):  # RR_TUNE_GEMM8 value (2: k_gemm8 wherever legal, persistent)
+        E.check(E.lib().rr_set_tuning(8, int(os.environ["G8"])), "rr_set_tuning")
     dt = torch.float16
     g = torch.Generator(device="cuda").manual_seed(1)
-    for (p, c, k) in ((4096, 4096, 4096), (8192, 8192, 8192), (16384, 4096, 2048), (393216, 256, 1024),
-                      (131072, 1024, 2048)):
+    shapes = ((4096, 4096, 4096), (8192, 8192, 8192), (16384, 4096, 2048), (393216, 256, 1024), (131072, 1024, 2048))
+    if os.environ.get("SHAPES"):
+        shapes = [tuple(int(v) for v in s.split("x")) for s in os.environ["SHAPES"].split(",")]
+    for (p, c, k) in shapes:
         hw = p
         x = (torch.rand(1, 1, hw, k, generator=g, device="cuda") * 2 - 1).to(dt)
         wt = (torch.rand(c, k, 1, 1, generator=g, device="cuda") * 2 - 1) / k ** 0.5
