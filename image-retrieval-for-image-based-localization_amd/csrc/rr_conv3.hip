@@ -46,7 +46,7 @@ __device__ __forceinline__ void pdma16(pi32x4_t rsrc, unsigned voff, unsigned ld
     asm volatile(
         "s_mov_b32 %0, m0\n\t"
         "s_mov_b32 m0, %3\n\t"
-        "s_nop 4\n\t"
+        "s_nop 0\n\t"  // M0 write -> LDS-DMA: 1 wait state (descriptor: fenced in the rsrc maker)
         "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
         "s_mov_b32 m0, %0"
         : "=&s"(keep)
@@ -77,6 +77,13 @@ __device__ __forceinline__ pi32x4_t prsrc(const void* base, unsigned bytes) {
     r.y = __builtin_amdgcn_readfirstlane((int)((unsigned)(b >> 32) & 0xFFFFu));
     r.z = __builtin_amdgcn_readfirstlane((int)bytes);
     r.w = 0x00020000;
+    // VALU (readfirstlane) SGPR write -> LDS-DMA descriptor read: 5 wait states, tied to the
+    // registers so no use of the descriptor is scheduled above it (tools/dma_audit.py checks)
+    int x = r.x, y = r.y, z = r.z;
+    asm volatile("s_nop 4" : "+s"(x), "+s"(y), "+s"(z));
+    r.x = x;
+    r.y = y;
+    r.z = z;
     return r;
 }
 
