@@ -35,9 +35,14 @@ def main():
     lab.lab_gemm4w.restype = ctypes.c_int
     lab.lab_gemm4w.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_int] * 3 + [ctypes.c_float, ctypes.c_int,
                                                                           ctypes.c_void_p]
+    g8modes = [int(v) for v in os.environ.get("G8MODES", "").split(",") if v]
+    if g8modes:
+        lab8 = ctypes.CDLL(os.path.join(HERE, "libg8lab.so"))
+        lab8.lab_g8.restype = ctypes.c_int
+        lab8.lab_g8.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_int] * 4 + [ctypes.c_void_p]
     if os.environ.get("G8"):
         E.check(E.lib().rr_set_tuning(8, int(os.environ["G8"])), "rr_set_tuning")
-    variants = [int(v) for v in os.environ.get("VARIANTS", "0").split(",")]
+    variants = [int(v) for v in os.environ.get("VARIANTS", "0").split(",") if v]
     shapes = ((16384, 4096, 2048), (8192, 8192, 8192), (131072, 1024, 2048), (393216, 256, 1024),
               (100352, 2048, 512))
     if os.environ.get("SHAPES"):
@@ -69,6 +74,16 @@ def main():
             err = (y4.float() - y8.float()).abs().max().item()
             line += " | v%d %.1f TF/s %s(maxdiff %.3g)" % (v, fl / timed(f4) / 1e12, "bit-identical " if same else "DIFFERS ",
                                                        err)
+        for md in g8modes:
+            y4 = torch.empty_like(y8)
+
+            def f8l():
+                rc = lab8.lab_g8(x.data_ptr(), wp.data_ptr(), one.data_ptr(), zero.data_ptr(), y4.data_ptr(), p, c, k, md, st)
+                assert rc == 0, rc
+            f8l()
+            torch.cuda.synchronize()
+            same = torch.equal(y4.view(torch.int16), y8.view(torch.int16))
+            line += " | g8lab m%d %.1f %s" % (md, fl / timed(f8l) / 1e12, "bit-identical" if same else "differs")
         print(line + " TF/s", flush=True)
         del x, wp, a, b, y8
 
