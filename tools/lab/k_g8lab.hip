@@ -7,6 +7,8 @@
 //   MODE 3: no barriers inside the K-loop       MODE 4: no s_setprio around the MFMA clusters
 //   MODE 5: both B halves' fragments held in registers: quadrant (1,0) reuses B0 instead of re-reading it
 //           (24 instead of 28 fragment reads per wave and K-step; bit-identical)
+//   MODE 6: the DMA issued but never waited for inside the K-loop (latency probe; wrong results)
+//   MODE 7: the K-loop's DMA issued with out-of-range offsets (issue + LDS writes of zeros, no memory reads)
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -shared -fPIC tools/lab/k_g8lab.hip -o tools/lab/libg8lab.so
 #include "../../image-retrieval-for-image-based-localization_amd/csrc/rr_internal.h"
 
@@ -87,7 +89,7 @@ __global__ void __launch_bounds__(512, 1) k_g8lab(G8Args a, int tiles_c, int nti
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const unsigned o = X < 2 ? a_off[X][i] : b_off[X - 2][i];
-            dma16(X < 2 ? rsA : rsB, live && o != OOB ? o + (unsigned)(kt * 128) : OOB, dst + (wave + 8 * i) * 1024);
+            dma16(X < 2 ? rsA : rsB, MODE != 7 && live && o != OOB ? o + (unsigned)(kt * 128) : OOB, dst + (wave + 8 * i) * 1024);
         }
     };
     f32x4_t acc[2][2][4][2];
@@ -143,7 +145,7 @@ __global__ void __launch_bounds__(512, 1) k_g8lab(G8Args a, int tiles_c, int nti
         if (MODE != 3) asm volatile("s_barrier" ::: "memory");
     };
     auto vm4 = []() {
-        if (MODE != 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        if (MODE != 1 && MODE != 6) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     };
     // prologue: K-step 0 into E (A0 B1 A1 B0), K-step 1's A0 / B1 into O
     {
@@ -239,6 +241,8 @@ extern "C" int lab_g8(const void* x, const void* w, const float* scale, const fl
         case 3: hipLaunchKernelGGL(lab8::k_g8lab<3>, dim3(ntiles), dim3(512), 0, s, a, tiles_c, ntiles); break;
         case 4: hipLaunchKernelGGL(lab8::k_g8lab<4>, dim3(ntiles), dim3(512), 0, s, a, tiles_c, ntiles); break;
         case 5: hipLaunchKernelGGL(lab8::k_g8lab<5>, dim3(ntiles), dim3(512), 0, s, a, tiles_c, ntiles); break;
+        case 6: hipLaunchKernelGGL(lab8::k_g8lab<6>, dim3(ntiles), dim3(512), 0, s, a, tiles_c, ntiles); break;
+        case 7: hipLaunchKernelGGL(lab8::k_g8lab<7>, dim3(ntiles), dim3(512), 0, s, a, tiles_c, ntiles); break;
         default: return -2;
     }
     return hipGetLastError() == hipSuccess ? 0 : -3;
