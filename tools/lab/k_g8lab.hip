@@ -9,6 +9,7 @@
 //           (24 instead of 28 fragment reads per wave and K-step; bit-identical)
 //   MODE 6: the DMA issued but never waited for inside the K-loop (latency probe; wrong results)
 //   MODE 7: the K-loop's DMA issued with out-of-range offsets (issue + LDS writes of zeros, no memory reads)
+//   MODE 8: every LDS-DMA with the nt bit, MODE 9: with sc1 (both bypass the CU's L1; bit-identical)
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -shared -fPIC tools/lab/k_g8lab.hip -o tools/lab/libg8lab.so
 #include "../../image-retrieval-for-image-based-localization_amd/csrc/rr_internal.h"
 
@@ -31,6 +32,21 @@ __device__ __forceinline__ void dma16(i32x4_t rsrc, unsigned voff, unsigned lds_
         : "=&s"(keep)
         : "v"(voff), "s"(rsrc), "s"(lds_addr)
         : "memory");
+}
+template <int POL>
+__device__ __forceinline__ void dma16p(i32x4_t rsrc, unsigned voff, unsigned lds_addr) {
+    if constexpr (POL == 0) {
+        dma16(rsrc, voff, lds_addr);
+    } else {
+        unsigned keep;
+        lds_addr = __builtin_amdgcn_readfirstlane(lds_addr);
+        if constexpr (POL == 1)
+            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen nt lds\n\t"
+                         "s_mov_b32 m0, %0" : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(lds_addr) : "memory");
+        else
+            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen sc1 lds\n\t"
+                         "s_mov_b32 m0, %0" : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(lds_addr) : "memory");
+    }
 }
 __device__ __forceinline__ i32x4_t make_rsrc(const void* base, unsigned bytes) {
     const unsigned long long b = (unsigned long long)base;
@@ -89,7 +105,7 @@ __global__ void __launch_bounds__(512, 1) k_g8lab(G8Args a, int tiles_c, int nti
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const unsigned o = X < 2 ? a_off[X][i] : b_off[X - 2][i];
-            dma16(X < 2 ? rsA : rsB, MODE != 7 && live && o != OOB ? o + (unsigned)(kt * 128) : OOB, dst + (wave + 8 * i) * 1024);
+            dma16p<MODE == 8 ? 1 : MODE == 9 ? 2 : 0>(X < 2 ? rsA : rsB, MODE != 7 && live && o != OOB ? o + (unsigned)(kt * 128) : OOB, dst + (wave + 8 * i) * 1024);
         }
     };
     f32x4_t acc[2][2][4][2];
@@ -243,6 +259,8 @@ extern "C" int lab_g8(const void* x, const void* w, const float* scale, const fl
         case 5: hipLaunchKernelGGL(lab8::k_g8lab<5>, dim3(ntiles), dim3(512), 0, s, a, tiles_c, ntiles); break;
         case 6: hipLaunchKernelGGL(lab8::k_g8lab<6>, dim3(ntiles), dim3(512), 0, s, a, tiles_c, ntiles); break;
         case 7: hipLaunchKernelGGL(lab8::k_g8lab<7>, dim3(ntiles), dim3(512), 0, s, a, tiles_c, ntiles); break;
+        case 8: hipLaunchKernelGGL(lab8::k_g8lab<8>, dim3(ntiles), dim3(512), 0, s, a, tiles_c, ntiles); break;
+        case 9: hipLaunchKernelGGL(lab8::k_g8lab<9>, dim3(ntiles), dim3(512), 0, s, a, tiles_c, ntiles); break;
         default: return -2;
     }
     return hipGetLastError() == hipSuccess ? 0 : -3;
