@@ -402,6 +402,130 @@ __global__ void __launch_bounds__(256, 1) k_gemm4w_v2(G4Args a, int tiles_c, int
     }
 }
 
+// VARIANT 3: register-staged loads instead of LDS-DMA, so the LDS writes happen where the schedule
+// puts them (phase A's first half) rather than whenever the DMA data arrives.  Per K-step kt:
+//   phase A: 16 groups {ds_write one staged 1-KiB piece of K-step kt+1 (groups 0-7: two), then the
+//            buffer loads of K-step kt+2 into the freed staging registers (groups 8-15: two),
+//            read one fragment of R1 (kt, hs 1), 4 MFMAs on R0}
+//   mid: lgkmcnt(0) + barrier (stage (kt+1)&1 written, stage kt&1 read)
+//   phase B: 16 groups {read one fragment of R0 (kt+1, hs 0) from stage (kt+1)&1, 4 MFMAs on R1}
+// The staging loads are compiler-visible (raw buffer loads), so hipcc places their vmcnt waits.
+__global__ void __launch_bounds__(256, 1) k_gemm4w_v3(G4Args a, int tiles_c, int ntiles) {
+    constexpr int HT = 16384, ST = 4 * HT;
+    __shared__ __attribute__((aligned(1024))) char smem[2 * ST];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = wave >> 1, wcl = wave & 1;
+    const int r16 = lane & 15, kq = lane >> 4;
+    const int lrow = lane >> 3, lch = lane & 7;
+    const int bx = (int)blockIdx.x, xcd = bx & 7, nt8 = ntiles >> 3, rt8 = ntiles & 7;
+    const int t = (xcd < rt8 ? xcd * (nt8 + 1) : rt8 * (nt8 + 1) + (xcd - rt8) * nt8) + (bx >> 3);
+    const int c0 = (t % tiles_c) * 256, p0 = (t / tiles_c) * 256;
+    const int K = a.K, nk = K / 64;
+    const int arows = min(256, a.C - c0);
+    __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)(a.w + (long long)c0 * K), (short)0,
+                                                                   arows * K * 2, 0x00020000);
+    __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.P * K * 2, 0x00020000);
+    // piece q (0..15) of a wave: half-tile X = q >> 2, rows (wave + 4 (q & 3)) * 8 + lrow, logical chunk lch
+    unsigned off[16];
+    int wofs[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int X = q >> 2, i = q & 3;
+        const int row = (X & 1) * 128 + (wave + 4 * i) * 8 + lrow;
+        if (X < 2) off[q] = row < arows ? (unsigned)((row * K + lch * 8) * 2) : OOB;
+        else off[q] = p0 + row < a.P ? (unsigned)(((p0 + row) * K + lch * 8) * 2) : OOB;
+        wofs[q] = X * HT + swz(row & 127, lch);
+    }
+    uint4 stg[16];
+    auto gload = [&](int q, int kt) {
+        const unsigned o = kt < nk && off[q] != OOB ? off[q] + (unsigned)(kt * 128) : OOB;
+        stg[q] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(q < 8 ? rsA : rsB, o, 0, 0));
+    };
+    auto swrite = [&](int q, int s) { *reinterpret_cast<uint4*>(smem + s * ST + wofs[q]) = stg[q]; };
+    f32x4_t acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    uint4 R0[16], R1[16];
+    auto rd1 = [&](uint4* R, int g, int s, int hs) {
+        const char* base = smem + s * ST + (g < 8 ? wr : 2 + wcl) * HT;
+        R[g] = *reinterpret_cast<const uint4*>(base + swz((g & 7) * 16 + r16, kq + 4 * hs));
+    };
+    auto mm4 = [&](const uint4* R, int g) {
+        const int i = g >> 1;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            const int j = 4 * (g & 1) + jj;
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, R[i]),
+                                                               __builtin_bit_cast(f16x8_t, R[8 + j]), acc[i][j], 0, 0, 0);
+        }
+    };
+    // prologue: K-step 0 staged and written to stage 0, K-step 1 staged
+#pragma unroll
+    for (int q = 0; q < 16; ++q) gload(q, 0);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) swrite(q, 0);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) gload(q, 1);
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < 16; ++g) rd1(R0, g, 0, 0);
+    for (int kt = 0; kt < nk; ++kt) {
+        const int s = kt & 1;
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+            __builtin_amdgcn_sched_barrier(0);
+            if (g < 8) {
+                swrite(2 * g, s ^ 1);
+                swrite(2 * g + 1, s ^ 1);
+            } else {
+                gload(2 * (g - 8), kt + 2);
+                gload(2 * (g - 8) + 1, kt + 2);
+            }
+            rd1(R1, g, s, 1);
+            mm4(R0, g);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+            __builtin_amdgcn_sched_barrier(0);
+            rd1(R0, g, s ^ 1, 0);
+            mm4(R1, g);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // the next phase A overwrites stage s (read in phase A above, fragments R1): every wave's
+        // reads of it are done (lgkmcnt(0) before the barrier above); stage s^1 (read in phase B)
+        // is written again only after the next mid barrier
+    }
+#pragma unroll
+    for (int i2 = 0; i2 < 4; ++i2) {
+        const int c = c0 + wr * 128 + 32 * i2 + 8 * kq;
+        if (c >= a.C) continue;
+        float sc[8], sh[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) { sc[r] = a.scale[c + r]; sh[r] = a.shift[c + r]; }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int p = p0 + wcl * 128 + j * 16 + r16;
+            if (p >= a.P) continue;
+            float v[8];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                v[r] = acc[2 * i2][j][r] * sc[r] + sh[r];
+                v[4 + r] = acc[2 * i2 + 1][j][r] * sc[4 + r] + sh[4 + r];
+            }
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * a.slope;
+            typedef __attribute__((ext_vector_type(8))) _Float16 h8;
+            *reinterpret_cast<h8*>(a.y + (long long)p * a.C + c) =
+                (h8){(f16_t)v[0], (f16_t)v[1], (f16_t)v[2], (f16_t)v[3], (f16_t)v[4], (f16_t)v[5], (f16_t)v[6], (f16_t)v[7]};
+        }
+    }
+}
+
 }  // namespace lab
 
 extern "C" int lab_gemm4w(const void* x, const void* w, const float* scale, const float* shift, void* y, int P, int C,
@@ -418,6 +542,7 @@ extern "C" int lab_gemm4w(const void* x, const void* w, const float* scale, cons
     else if (variant == 13) hipLaunchKernelGGL(lab::k_gemm4w_v1<3>, dim3(ntiles), dim3(256), 0, s, a, tiles_c, ntiles);
     else if (variant == 14) hipLaunchKernelGGL(lab::k_gemm4w_v1<4>, dim3(ntiles), dim3(256), 0, s, a, tiles_c, ntiles);
     else if (variant == 15) hipLaunchKernelGGL(lab::k_gemm4w_v1<5>, dim3(ntiles), dim3(256), 0, s, a, tiles_c, ntiles);
+    else if (variant == 3) hipLaunchKernelGGL(lab::k_gemm4w_v3, dim3(ntiles), dim3(256), 0, s, a, tiles_c, ntiles);
     else return -2;
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
