@@ -69,6 +69,7 @@ struct G8Args {
     const float *scale, *shift;
     f16_t* y;        // [P][C]
     int P, C, K;
+    unsigned long long* stamps;  // optional clock stamps [block][4]: memtime / memrealtime at start and end
 };
 
 template <int MODE>
@@ -88,6 +89,13 @@ __global__ void __launch_bounds__(512, 1) k_g8lab(G8Args a, int tiles_c, int nti
     const i32x4_t rsA = make_rsrc(a.w + (long long)c0 * K, (unsigned)((long long)arows * K * 2));
     const i32x4_t rsB = make_rsrc(a.x, (unsigned)((long long)a.P * K * 2));
     const unsigned lds0 = (unsigned)(unsigned long long)smem;
+    // clock stamps (diagnostic, separate buffer): wave 0 reads the shader clock and the constant
+    // reference clock before the prologue and after the K-loop
+    unsigned long long t0 = 0, r0 = 0;
+    if (a.stamps && wave == 0) {
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r0)::"memory");
+    }
     unsigned a_off[2][2], b_off[2][2];
 #pragma unroll
     for (int h = 0; h < 2; ++h)
@@ -213,6 +221,18 @@ __global__ void __launch_bounds__(512, 1) k_g8lab(G8Args a, int tiles_c, int nti
     }
     if (grp == 0) asm volatile("s_barrier" ::: "memory");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (a.stamps && wave == 0) {
+        unsigned long long t1, r1;
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r1)::"memory");
+        if (lane == 0) {
+            unsigned long long* st = a.stamps + 4ll * blockIdx.x;
+            st[0] = t0;
+            st[1] = r0;
+            st[2] = t1;
+            st[3] = r1;
+        }
+    }
 #pragma unroll
     for (int qa = 0; qa < 2; ++qa)
 #pragma unroll
@@ -244,10 +264,16 @@ __global__ void __launch_bounds__(512, 1) k_g8lab(G8Args a, int tiles_c, int nti
 
 }  // namespace lab8
 
+extern "C" int lab_g8s(const void* x, const void* w, const float* scale, const float* shift, void* y, int P, int C,
+                       int K, int mode, void* stream, unsigned long long* stamps);
 extern "C" int lab_g8(const void* x, const void* w, const float* scale, const float* shift, void* y, int P, int C,
                       int K, int mode, void* stream) {
+    return lab_g8s(x, w, scale, shift, y, P, C, K, mode, stream, nullptr);
+}
+extern "C" int lab_g8s(const void* x, const void* w, const float* scale, const float* shift, void* y, int P, int C,
+                       int K, int mode, void* stream, unsigned long long* stamps) {
     if (K % 128 || C % 32 || P <= 0) return -1;
-    lab8::G8Args a{(const rr::f16_t*)x, (const rr::f16_t*)w, scale, shift, (rr::f16_t*)y, P, C, K};
+    lab8::G8Args a{(const rr::f16_t*)x, (const rr::f16_t*)w, scale, shift, (rr::f16_t*)y, P, C, K, stamps};
     const int tiles_c = (C + 255) / 256, tiles_p = (P + 255) / 256, ntiles = tiles_c * tiles_p;
     hipStream_t s = (hipStream_t)stream;
     switch (mode) {
