@@ -18,7 +18,13 @@ def main():
     lab8 = ctypes.CDLL(os.path.join(HERE, "libg8lab.so"))
     lab8.lab_g8s.restype = ctypes.c_int
     lab8.lab_g8s.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_int] * 4 + [ctypes.c_void_p, ctypes.c_void_p]
-    modes = [int(v) for v in os.environ.get("MODES", "0,1,2,7").split(",")]
+    modes = [int(v) for v in os.environ.get("MODES", "0,1,2,7").split(",") if v]
+    lab4 = ctypes.CDLL(os.path.join(HERE, "libg4w.so"))
+    lab4.lab_gemm4ws.restype = ctypes.c_int
+    lab4.lab_gemm4ws.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_int] * 3 + [ctypes.c_float, ctypes.c_int,
+                                                                           ctypes.c_void_p, ctypes.c_void_p]
+    # 4-wave variants with stamps (variant 1 family: 15 = one-state DMA issue, 11 = no DMA in the K-loop)
+    variants = [int(v) for v in os.environ.get("VARIANTS", "").split(",") if v]
     shapes = [tuple(int(v) for v in s.split("x")) for s in
               os.environ.get("SHAPES", "16384x4096x2048,393216x256x1024").split(",")]
     dt = torch.float16
@@ -54,6 +60,26 @@ def main():
             ok = dt_ref > 0
             ghz = (dt_clk[ok] / dt_ref[ok] * 0.1).median().item()
             line += " | m%d %.1f TF/s, %.2f GHz" % (m, fl / t / 1e12, ghz)
+        for v in variants:
+            def run4(stamps):
+                rc = lab4.lab_gemm4ws(x.data_ptr(), wp.data_ptr(), one.data_ptr(), zero.data_ptr(), y.data_ptr(), p, c,
+                                      k, 1.0, v, st, stamps)
+                assert rc == 0, rc
+            for _ in range(3):
+                run4(None)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(10):
+                run4(st_buf.data_ptr())
+            e1.record()
+            torch.cuda.synchronize()
+            t = e0.elapsed_time(e1) / 10 * 1e-3
+            s = st_buf.view(ntiles, 4).cpu().double()
+            dt_clk, dt_ref = s[:, 2] - s[:, 0], s[:, 3] - s[:, 1]
+            ok = dt_ref > 0
+            ghz = (dt_clk[ok] / dt_ref[ok] * 0.1).median().item()
+            line += " | 4w-v%d %.1f TF/s, %.2f GHz" % (v, fl / t / 1e12, ghz)
         print(line, flush=True)
         del x, wp, y
 

@@ -70,6 +70,7 @@ struct G4Args {
     f16_t* y;         // [P][C]
     int P, C, K;
     float slope;
+    unsigned long long* stamps;  // optional clock stamps [block][4] (variant 1 only)
 };
 
 // VARIANT 0: 2 stages of a whole 64-deep K-step (4 half-tiles A0 A1 B0 B1, 64 KiB each); per
@@ -195,6 +196,11 @@ __global__ void __launch_bounds__(256, 1) k_gemm4w_v1(G4Args a, int tiles_c, int
     const i32x4_t rsA = make_rsrc(a.w + (long long)c0 * K, (unsigned)((long long)arows * K * 2));
     const i32x4_t rsB = make_rsrc(a.x, (unsigned)((long long)a.P * K * 2));
     const unsigned lds0 = (unsigned)(unsigned long long)smem;
+    unsigned long long t0 = 0, r0s = 0;
+    if (a.stamps && wave == 0) {
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r0s)::"memory");
+    }
     unsigned off[4][4];
 #pragma unroll
     for (int X = 0; X < 4; ++X)
@@ -261,6 +267,18 @@ __global__ void __launch_bounds__(256, 1) k_gemm4w_v1(G4Args a, int tiles_c, int
         __builtin_amdgcn_sched_barrier(0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (a.stamps && wave == 0) {
+        unsigned long long t1, r1;
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r1)::"memory");
+        if (lane == 0) {
+            unsigned long long* st = a.stamps + 4ll * blockIdx.x;
+            st[0] = t0;
+            st[1] = r0s;
+            st[2] = t1;
+            st[3] = r1;
+        }
+    }
 #pragma unroll
     for (int i2 = 0; i2 < 4; ++i2) {
         const int c = c0 + wr * 128 + 32 * i2 + 8 * kq;
@@ -528,10 +546,16 @@ __global__ void __launch_bounds__(256, 1) k_gemm4w_v3(G4Args a, int tiles_c, int
 
 }  // namespace lab
 
+extern "C" int lab_gemm4ws(const void* x, const void* w, const float* scale, const float* shift, void* y, int P,
+                           int C, int K, float slope, int variant, void* stream, unsigned long long* stamps);
 extern "C" int lab_gemm4w(const void* x, const void* w, const float* scale, const float* shift, void* y, int P, int C,
                           int K, float slope, int variant, void* stream) {
+    return lab_gemm4ws(x, w, scale, shift, y, P, C, K, slope, variant, stream, nullptr);
+}
+extern "C" int lab_gemm4ws(const void* x, const void* w, const float* scale, const float* shift, void* y, int P,
+                           int C, int K, float slope, int variant, void* stream, unsigned long long* stamps) {
     if (K % 64 || C % 32 || P <= 0) return -1;
-    lab::G4Args a{(const rr::f16_t*)x, (const rr::f16_t*)w, scale, shift, (rr::f16_t*)y, P, C, K, slope};
+    lab::G4Args a{(const rr::f16_t*)x, (const rr::f16_t*)w, scale, shift, (rr::f16_t*)y, P, C, K, slope, stamps};
     const int tiles_c = (C + 255) / 256, tiles_p = (P + 255) / 256, ntiles = tiles_c * tiles_p;
     hipStream_t s = (hipStream_t)stream;
     if (variant == 0) hipLaunchKernelGGL((lab::k_gemm4w<0>), dim3(ntiles), dim3(256), 0, s, a, tiles_c, ntiles);
